@@ -1,0 +1,198 @@
+"""Generate the golden vectors under tests/golden/ by running the REFERENCE itself on CPU.
+
+Run in the build container (where /root/reference exists):
+    python tests/golden/make_golden.py
+
+Recipe: put /root/reference on sys.path with bytecode writing disabled, stub the
+unused `comet_ml` / `torchvision` imports of models/mm_transformers.py:2-3,14-15, patch
+Tensor.cuda to identity while losses/loss.py:16 builds its bins, overwrite every parameter with
+the counter-hash values of oracle/hashinit.py, run forward + backward, save small .npz fixtures.
+Inputs are NOT stored: they are regenerated from the same hash (oracle/hashinit.features/labels);
+a checksum of each input is stored so a drifting generator is caught.
+
+The reference's sources never leave this script: the fixtures are data (outputs, losses, grad
+norms and strided grad samples).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+from oracle import hashinit as hi  # noqa: E402
+from tests.golden import spec  # noqa: E402
+
+REF = "/root/reference"
+N_SAMPLE = spec.N_SAMPLE
+
+
+def import_reference():
+    sys.dont_write_bytecode = True
+    for name in ("comet_ml",):
+        m = types.ModuleType(name)
+        m.Experiment = object
+        sys.modules[name] = m
+    tv = types.ModuleType("torchvision")
+    tv.transforms = types.ModuleType("torchvision.transforms")
+    tv.models = types.ModuleType("torchvision.models")
+    tv.models.video = types.ModuleType("torchvision.models.video")
+    tv.models.video.r3d_18 = None
+    for k, v in {"torchvision": tv, "torchvision.transforms": tv.transforms,
+                 "torchvision.models": tv.models,
+                 "torchvision.models.video": tv.models.video}.items():
+        sys.modules[k] = v
+    sys.path.insert(0, REF)
+    import importlib
+    mods = {}
+    for name in ("models.two_transformers", "models.fc_layer", "models.mm_multi_transformers",
+                 "models.mm_transformers", "models.intra_modal_transformer_fusion",
+                 "losses.loss", "losses.CCCLoss"):
+        mods[name] = importlib.import_module(name)
+    return mods
+
+
+def make_loss(mods, cls, *a, **k):
+    orig = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *x, **y: self
+    try:
+        return getattr(mods["losses.loss"], cls)(*a, **k)
+    finally:
+        torch.Tensor.cuda = orig
+
+
+def grad_record(out: dict, tag: str, named):
+    for name, t in named:
+        g = t.grad
+        key = f"{tag}/{name}"
+        if g is None:
+            out[key + ":norm"] = np.array(-1.0)
+            continue
+        g = g.detach().double().reshape(-1)
+        out[key + ":norm"] = np.array(float(g.norm()))
+        stride = max(1, g.numel() // N_SAMPLE)
+        out[key + ":sample"] = g[::stride][:N_SAMPLE].float().numpy()
+
+
+def checksum(x: np.ndarray) -> float:
+    return float(np.float64(x).sum() + (np.float64(x) ** 2).sum())
+
+
+def run_two_transformers(mods, out, c):
+    tag = c["tag"]
+    torch.manual_seed(0)
+    model = mods["models.two_transformers"].Two_transformers(
+        0.0, 0.0, c["H"], c["L"], c["jm"], c["fmt"], c["vin"])
+    fc = mods["models.fc_layer"].FcLayer(1024, 512)
+    hi.init_module_(model, "")
+    hi.init_module_(fc, "fc.")
+    model.train()
+    B, T = c["B"], c["T"]
+    audio, video, lv, la = spec.tt_inputs(tag, B, T, c["vin"])
+    out[f"{tag}/in_checksum"] = np.array([checksum(audio), checksum(video), checksum(lv),
+                                          checksum(la)])
+    a = torch.from_numpy(audio).requires_grad_(True)
+    v = torch.from_numpy(video).requires_grad_(True)
+    crit = make_loss(mods, "CCCLoss", 1)
+    aud = fc(a)
+    vo, ao = model(aud, v)
+    out[f"{tag}/vouts"] = vo.detach().numpy()
+    out[f"{tag}/aouts"] = ao.detach().numpy()
+    vout = vo.view(-1, vo.shape[0] * vo.shape[1])
+    aout = ao.view(-1, ao.shape[0] * ao.shape[1])
+    vt = torch.from_numpy(lv).view(-1, B * T)
+    at = torch.from_numpy(la).view(-1, B * T)
+    l1 = crit(vout, vt)
+    l2 = crit(aout, at)
+    out[f"{tag}/v_loss"] = np.array(float(l1))
+    out[f"{tag}/a_loss"] = np.array(float(l2))
+    (l1 + l2).backward()
+    grad_record(out, tag, list(model.named_parameters()))
+    grad_record(out, tag, [("fc." + n, p) for n, p in fc.named_parameters()])
+    grad_record(out, tag, [("input.audio", a), ("input.video", v)])
+
+    if c.get("train_steps"):
+        # 3-step training trajectory (SURVEY.md §8c last paragraph): SGD nesterov, config lr etc.
+        params = list(model.parameters()) + list(fc.parameters())
+        opt = torch.optim.SGD(params, lr=1e-4, momentum=0.9, dampening=0.0, weight_decay=1e-4,
+                              nesterov=True)
+        losses = []
+        for step in range(c["train_steps"]):
+            opt.zero_grad(set_to_none=True)
+            vo, ao = model(fc(torch.from_numpy(audio)), torch.from_numpy(video))
+            l1 = crit(vo.view(-1, B * T), vt)
+            l2 = crit(ao.view(-1, B * T), at)
+            (l1 + l2).backward()
+            opt.step()
+            losses.append([float(l1), float(l2)])
+        out[f"{tag}/train_losses"] = np.array(losses)
+        out[f"{tag}/train_final_out_layer1_w_sample"] = (
+            model.mm_transformer.out_layer1.weight.detach().reshape(-1)[:N_SAMPLE].numpy())
+
+
+def run_intra(mods, out, c):
+    tag = c["tag"]
+    m = mods["models.intra_modal_transformer_fusion"].Intra_modal_transformer_fusion(
+        512, c["H"], 512, c["L"])
+    hi.init_module_(m, "intra.")
+    fa_np, fb_np, w_np = spec.intra_inputs(tag, c["B"], c["T"], c["Da"], c["Db"])
+    fa = torch.from_numpy(fa_np).requires_grad_(True)
+    fb = torch.from_numpy(fb_np).requires_grad_(True)
+    o = m(fa, fb)
+    out[f"{tag}/out"] = o.detach().numpy()
+    (o * torch.from_numpy(w_np)).sum().backward()
+    grad_record(out, tag, list(m.named_parameters()))
+    grad_record(out, tag, [("input.a", fa), ("input.b", fb)])
+
+
+def run_losses(mods, out):
+    CCCi = mods["losses.CCCLoss"].CCCLoss
+    for case in spec.LOSS_CASES:
+        tag = case["tag"]
+        x_np, y_np = spec.loss_inputs(case)
+        x = torch.from_numpy(x_np).requires_grad_(True)
+        y = torch.from_numpy(y_np)
+        if case["kind"] == "ccc":
+            crit = make_loss(mods, "CCCLoss", case["k"])
+            l = crit(x, y)
+        elif case["kind"] == "ccc_ignore":
+            l = CCCi(ignore=-5.0)(x, y)
+            out[f"{tag}/mask_idx"] = np.nonzero(y_np.reshape(-1) != -5.0)[0].astype(np.int64)
+        elif case["kind"] == "ce":
+            crit = make_loss(mods, "CELoss", case["k"])
+            orig = torch.cuda.LongTensor
+            try:
+                torch.cuda.LongTensor = lambda a: torch.as_tensor(a, dtype=torch.long)
+                l = crit(x, y)
+            finally:
+                torch.cuda.LongTensor = orig
+        out[f"{tag}/loss"] = np.array(float(l))
+        if l.requires_grad:
+            l.backward()
+        out[f"{tag}/grad"] = (x.grad.numpy() if x.grad is not None
+                              else np.zeros_like(x_np))
+
+
+def main():
+    mods = import_reference()
+    torch.set_num_threads(8)
+    out = {}
+    for c in spec.TT_CASES:
+        print("case", c["tag"], flush=True)
+        run_two_transformers(mods, out, c)
+    for c in spec.INTRA_CASES:
+        print("case", c["tag"], flush=True)
+        run_intra(mods, out, c)
+    run_losses(mods, out)
+    path = os.path.join(HERE, "golden.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,105 @@
+"""Run the golden cases through the CPU oracle and compare results with the golden fixtures.
+Shared by tests/test_oracle.py (oracle vs reference-generated goldens)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from oracle import jmt_ref as R
+from tests.golden import spec
+
+
+def rel_err(a, b) -> float:
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    den = max(np.abs(b).max(), 1e-30)
+    return float(np.abs(a - b).max() / den)
+
+
+def oracle_tt(c: dict) -> dict:
+    tag = c["tag"]
+    shapes = R.two_transformers_shapes(c["L"], c["jm"], c["fmt"], c["vin"])
+    p = R.hash_params(shapes, "")
+    fcp = R.hash_params({"fc_layer.weight": (512, 1024), "fc_layer.bias": (512,)}, "fc.")
+    B, T = c["B"], c["T"]
+    audio, video, lv, la = spec.tt_inputs(tag, B, T, c["vin"])
+    for t in list(p.values()) + list(fcp.values()):
+        t.requires_grad_(True)
+    a = torch.from_numpy(audio).requires_grad_(True)
+    v = torch.from_numpy(video).requires_grad_(True)
+    aud = R.linear(a, fcp["fc_layer.weight"], fcp["fc_layer.bias"])
+    vo, ao = R.two_transformers_forward(aud, v, p, c["H"], c["L"], c["jm"], c["fmt"], c["vin"])
+    l1 = R.ccc_loss(vo.reshape(1, -1), torch.from_numpy(lv).reshape(1, -1))
+    l2 = R.ccc_loss(ao.reshape(1, -1), torch.from_numpy(la).reshape(1, -1))
+    (l1 + l2).backward()
+    res = {"vouts": vo.detach().numpy(), "aouts": ao.detach().numpy(),
+           "v_loss": float(l1), "a_loss": float(l2), "grads": {}}
+    for k, t in p.items():
+        res["grads"][k] = t.grad
+    for k, t in fcp.items():
+        res["grads"]["fc." + k] = t.grad
+    res["grads"]["input.audio"] = a.grad
+    res["grads"]["input.video"] = v.grad
+    return res
+
+
+def compare_grads(golden: dict, tag: str, grads: dict, tol: float):
+    """Every parameter: relative L2-norm error and the strided sample; None grads must be None."""
+    bad = []
+    scale = max(float(v) for k, v in golden.items()
+                if k.startswith(tag + "/") and k.endswith(":norm"))
+    atol = 0.1 * tol * scale   # cancellation-dominated sums (e.g. last-layer bias grads)
+    for name, g in grads.items():
+        key = f"{tag}/{name}"
+        gn = float(golden[key + ":norm"])
+        if gn < 0:
+            if g is not None and float(torch.as_tensor(g).abs().max()) != 0.0:
+                bad.append((name, "expected no grad"))
+            continue
+        if g is None:
+            bad.append((name, "missing grad"))
+            continue
+        g = torch.as_tensor(g).detach().double().cpu().reshape(-1)
+        n = float(g.norm())
+        if abs(n - gn) > tol * gn + atol:
+            bad.append((name, f"norm {n} vs {gn}"))
+            continue
+        stride = max(1, g.numel() // spec.N_SAMPLE)
+        s = g[::stride][:spec.N_SAMPLE].numpy()
+        ref = golden[key + ":sample"]
+        err = np.abs(s - ref).max()
+        if err > 10 * tol * max(np.abs(ref).max(), gn / np.sqrt(g.numel())) + atol:
+            bad.append((name, f"sample rel err {err}"))
+    return bad
+
+
+def oracle_intra(c: dict) -> dict:
+    tag = c["tag"]
+    p = R.hash_params(R.intra_modal_shapes(512, c["L"]), "intra.")
+    for t in p.values():
+        t.requires_grad_(True)
+    fa_np, fb_np, w_np = spec.intra_inputs(tag, c["B"], c["T"], c["Da"], c["Db"])
+    fa = torch.from_numpy(fa_np).requires_grad_(True)
+    fb = torch.from_numpy(fb_np).requires_grad_(True)
+    o = R.intra_modal_forward(fa, fb, p, "", c["H"], c["L"])
+    (o * torch.from_numpy(w_np)).sum().backward()
+    grads = {k: t.grad for k, t in p.items()}
+    grads["input.a"] = fa.grad
+    grads["input.b"] = fb.grad
+    return {"out": o.detach().numpy(), "grads": grads}
+
+
+def oracle_loss(case: dict):
+    x_np, y_np = spec.loss_inputs(case)
+    x = torch.from_numpy(x_np).requires_grad_(True)
+    y = torch.from_numpy(y_np)
+    if case["kind"] == "ccc":
+        l = R.ccc_loss(x, y, digitize_num=case["k"])
+    elif case["kind"] == "ccc_ignore":
+        l = R.ccc_loss_ignore(x, y)
+    else:
+        l = R.ce_loss(x, y, case["k"])
+    if l.requires_grad:
+        l.backward()
+    g = x.grad.numpy() if x.grad is not None else np.zeros_like(x_np)
+    return float(l), g
