@@ -1,0 +1,162 @@
+/*
+ * jmt.h — C-ABI of libjmt_hip.so, the MI355X (gfx950) kernels of the Joint-Multimodal-Transformer
+ * fusion hot path.
+ *
+ * The reference (PoloWlg/Joint-Multimodal-Transformer-6th-ABAW) has no FFI: its boundary is Python
+ * module/class identity.  The Python drop-in modules under
+ * joint-multimodal-transformer-6th-abaw_amd/{models,losses} bind these entry points with ctypes
+ * (jmt/_lib.py); each entry point replaces the stock PyTorch op(s) the reference calls at the
+ * cited lines.  Conventions:
+ *   - every pointer is a device pointer owned by the caller (the PyTorch caching allocator),
+ *     including workspaces; the library never allocates device memory and keeps no state;
+ *   - every call is enqueued on `stream` (a hipStream_t); no host synchronisation;
+ *   - return 0 on success or a negative JMT_ERR_*; jmt_last_error() describes the last failure
+ *     (thread-local).
+ */
+#ifndef JMT_H_
+#define JMT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JMT_ABI_VERSION 1
+
+enum { JMT_F32 = 0, JMT_BF16 = 1, JMT_F16 = 2 };
+enum { JMT_OK = 0, JMT_ERR_ARG = -1, JMT_ERR_HIP = -2, JMT_ERR_UNSUPPORTED = -3 };
+
+int jmt_abi_version(void);
+const char* jmt_last_error(void);
+/* number of gfx950 code objects / kernels compiled in (sanity probe, no GPU needed) */
+int jmt_kernel_count(void);
+
+/* ------------------------------------------------------------------ GEMM
+ * C[b] = epilogue(alpha * A[b] . B[b]),  A: M x K, B: K x N, C: M x N.
+ *   a_kmajor=1: A[m][k] at a + m*lda + k   (row-major activations)      a_kmajor=0: a + k*lda + m
+ *   b_kmajor=1: B[k][n] at b + n*ldb + k   (nn.Linear weight, W^T)      b_kmajor=0: b + k*ldb + n
+ * batch index b = (b0, b1), b0 < batch0, b1 < batch1.  Operand address modes:
+ *   0 strided:   base[0] + b0*s0 + b1*s1
+ *   1 table:     base[b0] + b1*s1                        (up to 8 tensors)
+ *   2 K-concat:  K range [i*kseg, (i+1)*kseg) read from base[i]  (a torch.cat along the feature
+ *                axis that is never materialised; kseg a multiple of 64 (16-bit) / 32 (f32))
+ * Epilogue on the fp32 accumulator: *alpha, +bias (1: per column n, 2: per row m), +beta*C,
+ * ReLU, then zeroed where aux <= 0 (ReLU backward mask), stored as c_dtype.
+ * splits > 1: split-K with fp32 partial slabs in `workspace` (jmt_gemm_workspace_bytes), then a
+ * deterministic reduce + epilogue launch.
+ * Replaces: nn.Linear (fc_layer.py:6-12, two_transformers.py:56,104-114,
+ * mm_multi_transformers.py:52-56,99,102), the in_proj/out_proj GEMMs and the bmm's of
+ * F.multi_head_attention_forward behind every nn.MultiheadAttention, and
+ * their autograd backward.
+ */
+typedef struct jmt_gemm_desc {
+  int ab_dtype, c_dtype, aux_dtype;
+  int M, N, K;
+  const void* a[8];
+  const void* b[8];
+  void* c[8];
+  int n_a, n_b, n_c;
+  int a_mode, b_mode, c_mode;
+  int a_kseg, b_kseg;
+  int a_kmajor, b_kmajor;
+  int64_t lda, ldb, ldc, ldaux;
+  int batch0, batch1;
+  int64_t sA0, sA1, sB0, sB1, sC0, sC1;
+  float alpha, beta;
+  const float* bias;
+  int bias_mode;
+  int relu;
+  const void* aux;
+  int splits;
+  void* workspace;
+  size_t ws_bytes;
+} jmt_gemm_desc;
+
+int jmt_gemm(const jmt_gemm_desc* desc, void* stream);
+size_t jmt_gemm_workspace_bytes(int M, int N, int batch, int splits);
+
+/* ------------------------------------------------------------------ row-wise ops
+ * Rows are `rows` vectors of length D at stride ld (elements). */
+
+/* F.normalize(x, p=2, dim=-1, eps) (two_transformers.py:118-119): y = x / max(||x||, eps);
+ * writes inv_norm[r] = 1 / max(||x_r||, eps) (fp32) for the backward. */
+int jmt_l2norm_fwd(int x_dt, int y_dt, int64_t rows, int D, const void* x, int64_t ldx, void* y,
+                   int64_t ldy, float* inv_norm, float eps, void* stream);
+/* dx = (dy - y (y.dy)) * inv_norm when ||x|| > eps, else dy * inv_norm;  y = x * inv_norm. */
+int jmt_l2norm_bwd(int x_dt, int dy_dt, int dx_dt, int64_t rows, int D, const void* x,
+                   int64_t ldx, const void* dy, int64_t lddy, const float* inv_norm, float eps,
+                   void* dx, int64_t lddx, void* stream);
+
+/* Post-LN residual block (mm_multi_transformers.py:64-70): y = LayerNorm(x + r) * gamma + beta,
+ * eps, biased variance.  r may be NULL.  Saves mean / rstd (fp32, per row). */
+int jmt_layernorm_fwd(int dt_in, int dt_out, int64_t rows, int D, const void* x, int64_t ldx,
+                      const void* r, int64_t ldr, const float* gamma, const float* beta, float eps,
+                      void* y, int64_t ldy, float* mean, float* rstd, void* stream);
+/* ds = d(x+r); dgamma/dbeta accumulated as fp32 partial slabs into `partials` (2 * nblk * D
+ * floats, nblk = jmt_layernorm_bwd_blocks(rows)) and reduced into dgamma/dbeta (beta_acc=1 adds
+ * to the existing values). */
+int jmt_layernorm_bwd_blocks(int64_t rows);
+int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, int D, const void* x,
+                      int64_t ldx, const void* r, int64_t ldr, const void* dy, int64_t lddy,
+                      const float* mean, const float* rstd, const float* gamma, void* dx,
+                      int64_t lddx, float* dgamma, float* dbeta, int beta_acc, float* partials,
+                      void* stream);
+
+/* Attention softmax (F.multi_head_attention_forward): rows of length n of the
+ * fp32 score matrix S (ld) -> P = softmax(scale * S) stored as p_dt at ldp; columns [n, ldp)
+ * of P are zeroed. */
+int jmt_softmax_fwd(int p_dt, int64_t rows, int n, const float* s, int64_t lds, float scale,
+                    void* p, int64_t ldp, void* stream);
+/* dS = scale * P o (dP - rowsum(P o dP)), dP fp32, dS stored as ds_dt (columns [n, ldds) = 0). */
+int jmt_softmax_bwd(int p_dt, int ds_dt, int64_t rows, int n, const void* p, int64_t ldp,
+                    const float* dp, int64_t lddp, float scale, void* ds, int64_t ldds,
+                    void* stream);
+
+/* Bias gradient: db[n] (+)= sum_m dy[m][n] (two-phase, deterministic, fp32 partial slabs of
+ * jmt_colsum_blocks(rows) * N floats). */
+int jmt_colsum_blocks(int64_t rows);
+int jmt_colsum(int dt, int64_t rows, int N, const void* dy, int64_t ld, float* db, int beta_acc,
+               float* partials, void* stream);
+
+/* Strided 2-D copy with dtype conversion and optional transpose (layout plumbing:
+ * the (T,B) output of the FC head, torch.stack of the SELF_ATTEN head). dst may be accumulated
+ * into (accumulate=1). */
+int jmt_copy2d(int src_dt, int dst_dt, int64_t rows, int64_t cols, const void* src,
+               int64_t src_rs, int64_t src_cs, void* dst, int64_t dst_rs, int64_t dst_cs,
+               int accumulate, void* stream);
+
+/* ------------------------------------------------------------------ CCC losses
+ * kind 0: losses/loss.py:8-32 CCCLoss (digitize_num k; k>1: pred is (n,k) logits, softmax over
+ *         bins = linspace(range) first)
+ * kind 1: losses/CCCLoss.py:4-43 CCCLoss(ignore) (labels == ignore are masked; the ccc is
+ *         divided by the pre-mask batch size `bs`)
+ * Local statistics (double[8]: n, mean_x, mean_y, M2x, M2y, Cxy, 0, 0) of this rank's elements;
+ * several ranks' statistics are combined exactly (Chan) by jmt_ccc_finish, which writes the loss
+ * (fp32 scalar) and 8 doubles of gradient coefficients {c0, c1, c2, mean_x, mean_y, valid, 0, 0}
+ * used by jmt_ccc_bwd: dL/dx_i = grad_loss * (c0 + c1 (x_i - mean_x) + c2 (y_i - mean_y)). */
+int jmt_ccc_stats(int kind, int pred_dt, int64_t n, int k, const void* pred, const float* label,
+                  float ignore, float lo, float hi, double* stats, void* stream);
+int jmt_ccc_finish(int kind, int world, const double* stats_all, int64_t bs, float eps,
+                   float* loss, double* coef, void* stream);
+int jmt_ccc_bwd(int kind, int pred_dt, int64_t n, int k, const void* pred, const float* label,
+                float ignore, float lo, float hi, const double* coef, const float* grad_loss,
+                void* dpred, void* stream);
+/* Mask indices (labels != ignore) in ascending order, count written to *count (device int64).
+ * The bit-exact padding-mask indices of the ignore path. */
+int jmt_mask_indices(int64_t n, const float* label, float ignore, int64_t* idx, int64_t* count,
+                     void* stream);
+
+/* ------------------------------------------------------------------ optimizer
+ * torch.optim.SGD(momentum, dampening, weight_decay, nesterov) step over one flat fp32 buffer
+ * (instantiator.py:32-38).  grad is multiplied by grad_scale first (GradScaler unscale); if
+ * shadow != NULL the updated params are also written as shadow_dt (bf16/f16 compute copies). */
+int jmt_sgd_step(int64_t n, float* param, const float* grad, float* momentum_buf, float lr,
+                 float momentum, float dampening, float weight_decay, int nesterov,
+                 int first_step, float grad_scale, void* shadow, int shadow_dt, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JMT_H_ */

@@ -1,0 +1,290 @@
+// Concordance-correlation-coefficient losses of the JMT path (losses/loss.py:8-32 and
+// losses/CCCLoss.py:4-43), forward + analytic backward, with rank-local sufficient statistics
+// that combine exactly across data-parallel ranks (Chan et al. pairwise update) so the loss stays
+// a GLOBAL-batch statistic as it is under the reference's DataParallel gather.
+//
+// Statistics are accumulated in double (one 1024-thread block; n = B*T elements per rank, a few
+// 10^4) — the kernel is latency-bound, never bandwidth-bound.
+#include "common.h"
+
+namespace jmt {
+
+constexpr int CT = 1024;
+constexpr int MAXK = 64;   // digitize_num bins
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  v = wave_sum_d(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < CT / 64; ++i) s += red[i];
+  __syncthreads();
+  return s;
+}
+
+// numpy.linspace(lo, hi, k)[c] in float64, then cast to float32 (loss.py:14-16)
+__device__ __forceinline__ float bin_value(int c, int k, float lo, float hi) {
+  if (k == 1) return lo;
+  const double step = ((double)hi - (double)lo) / (double)(k - 1);
+  double v = (double)lo + (double)c * step;
+  if (c == k - 1) v = hi;
+  return (float)v;
+}
+
+// prediction value of element i: the raw prediction (k == 1) or sum_c softmax(z_i)_c * bins_c
+template <typename T>
+__device__ __forceinline__ float pred_value(const T* pred, int64_t i, int k, float lo, float hi) {
+  if (k == 1) return to_f(pred[i]);
+  const T* z = pred + i * k;
+  float m = -INFINITY;
+  for (int c = 0; c < k; ++c) m = fmaxf(m, to_f(z[c]));
+  float s = 0.f, e = 0.f;
+  for (int c = 0; c < k; ++c) {
+    const float p = __expf(to_f(z[c]) - m);
+    s += p;
+    e += p * bin_value(c, k, lo, hi);
+  }
+  return e / s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(CT) void ccc_stats_kernel(int kind, int64_t n, int k, const T* pred,
+                                                       const float* label, float ignore, float lo,
+                                                       float hi, double* stats) {
+  __shared__ double red[CT / 64];
+  double c = 0, sx = 0, sy = 0;
+  for (int64_t i = threadIdx.x; i < n; i += CT) {
+    const float y = label[i];
+    if (kind == 1 && y == ignore) continue;
+    c += 1.0;
+    sx += pred_value(pred, i, k, lo, hi);
+    sy += y;
+  }
+  c = block_sum_d(c, red);
+  sx = block_sum_d(sx, red);
+  sy = block_sum_d(sy, red);
+  const double mx = c > 0 ? sx / c : 0.0, my = c > 0 ? sy / c : 0.0;
+  double xx = 0, yy = 0, xy = 0;
+  for (int64_t i = threadIdx.x; i < n; i += CT) {
+    const float y = label[i];
+    if (kind == 1 && y == ignore) continue;
+    const double dx = (double)pred_value(pred, i, k, lo, hi) - mx, dy = (double)y - my;
+    xx += dx * dx;
+    yy += dy * dy;
+    xy += dx * dy;
+  }
+  xx = block_sum_d(xx, red);
+  yy = block_sum_d(yy, red);
+  xy = block_sum_d(xy, red);
+  if (threadIdx.x == 0) {
+    stats[0] = c; stats[1] = mx; stats[2] = my;
+    stats[3] = xx; stats[4] = yy; stats[5] = xy;
+    stats[6] = 0; stats[7] = 0;
+  }
+}
+
+// Combine rank statistics in fixed rank order, then loss + gradient coefficients.
+//   coef = {c0, c1, c2, mean_x, mean_y, valid, 0, 0};  dL/dx_i = c0 + c1 (x_i - mx) + c2 (y_i - my)
+__global__ void ccc_finish_kernel(int kind, int world, const double* st, int64_t bs, float eps,
+                                  float* loss, double* coef) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double n = st[0], mx = st[1], my = st[2], Sxx = st[3], Syy = st[4], Sxy = st[5];
+  for (int r = 1; r < world; ++r) {
+    const double* s = st + 8 * r;
+    const double nb = s[0];
+    if (nb <= 0) continue;
+    if (n <= 0) { n = nb; mx = s[1]; my = s[2]; Sxx = s[3]; Syy = s[4]; Sxy = s[5]; continue; }
+    const double nt = n + nb, dx = s[1] - mx, dy = s[2] - my, f = n * nb / nt;
+    Sxx += s[3] + dx * dx * f;
+    Syy += s[4] + dy * dy * f;
+    Sxy += s[5] + dx * dy * f;
+    mx += dx * nb / nt;
+    my += dy * nb / nt;
+    n = nt;
+  }
+  for (int i = 0; i < 8; ++i) coef[i] = 0.0;
+  coef[3] = mx;
+  coef[4] = my;
+  if (kind == 0) {
+    // losses/loss.py:23-32 in fp32 op order (rho with eps, unbiased std, no eps in the ccc)
+    const float fn = (float)n;
+    const float sxx = (float)Sxx, syy = (float)Syy, sxy = (float)Sxy;
+    const float a = sqrtf(sxx), b = sqrtf(syy);
+    const float q = a * b + eps;
+    const float rho = sxy / q;
+    const float xs = sqrtf(sxx / (fn - 1.f)), ys = sqrtf(syy / (fn - 1.f));
+    const float dmean = (float)mx - (float)my;
+    const float den = xs * xs + ys * ys + dmean * dmean;
+    const float ccc = 2.f * rho * xs * ys / den;
+    *loss = 1.f - ccc;
+    // analytic gradient in double
+    const double nm1 = n - 1.0;
+    const double A = sqrt(Sxx), Bv = sqrt(Syy), Q = A * Bv + (double)eps;
+    const double num = 2.0 * Sxy * A * Bv / (nm1 * Q);
+    const double D = (Sxx + Syy) / nm1 + (mx - my) * (mx - my);
+    const double dnum_dSxy = 2.0 * A * Bv / (nm1 * Q);
+    const double dnum_dSxx = A > 0 ? Sxy * Bv * (double)eps / (nm1 * Q * Q * A) : 0.0;
+    const double dccc_dSxy = dnum_dSxy / D;
+    const double dccc_dSxx = dnum_dSxx / D - num / (D * D) / nm1;
+    const double dccc_dmx = -num / (D * D) * 2.0 * (mx - my);
+    coef[0] = -dccc_dmx / n;
+    coef[1] = -2.0 * dccc_dSxx;
+    coef[2] = -dccc_dSxy;
+    coef[5] = 1.0;
+  } else {
+    // losses/CCCLoss.py:24-43: masked compaction, <=1 element -> 0; std names swapped;
+    // ccc = 2 s_xy / ((std(t)^2 + std(p)^2 + (mp - mt)^2 + 1e-8) * bs)
+    if (n <= 1.0) {
+      *loss = 0.f;
+      return;
+    }
+    const float fn = (float)n;
+    const float x_std = sqrtf((float)Syy / (fn - 1.f));   // std(y_true)
+    const float y_std = sqrtf((float)Sxx / (fn - 1.f));   // std(y_pred)
+    const float dm = (float)mx - (float)my;
+    const float den = x_std * x_std + y_std * y_std + dm * dm + 1e-8f;
+    const float ccc = 2.f * (float)Sxy / (den * (float)bs);
+    *loss = 1.f - ccc;
+    const double nm1 = n - 1.0;
+    const double D = Syy / nm1 + Sxx / nm1 + (mx - my) * (mx - my) + 1e-8;
+    const double dccc_dSxy = 2.0 / (D * (double)bs);
+    const double g = -2.0 * Sxy / (D * D * (double)bs);
+    const double dccc_dSxx = g / nm1;
+    const double dccc_dmx = g * 2.0 * (mx - my);
+    coef[0] = -dccc_dmx / n;
+    coef[1] = -2.0 * dccc_dSxx;
+    coef[2] = -dccc_dSxy;
+    coef[5] = 1.0;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ccc_bwd_kernel(int kind, int64_t n, int k, const T* pred,
+                                                      const float* label, float ignore, float lo,
+                                                      float hi, const double* coef,
+                                                      const float* grad_loss, T* dpred) {
+  const double c0 = coef[0], c1 = coef[1], c2 = coef[2], mx = coef[3], my = coef[4];
+  const bool valid = coef[5] != 0.0;
+  const float g = grad_loss ? *grad_loss : 1.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float y = label[i];
+    const bool masked = !valid || (kind == 1 && y == ignore);
+    if (k == 1) {
+      float d = 0.f;
+      if (!masked) {
+        const double x = to_f(pred[i]);
+        d = (float)((c0 + c1 * (x - mx) + c2 * ((double)y - my)) * (double)g);
+      }
+      dpred[i] = from_f<T>(d);
+    } else {
+      const T* z = pred + i * k;
+      T* dz = dpred + i * k;
+      if (masked) {
+        for (int c = 0; c < k; ++c) dz[c] = from_f<T>(0.f);
+        continue;
+      }
+      float m = -INFINITY;
+      for (int c = 0; c < k; ++c) m = fmaxf(m, to_f(z[c]));
+      float s = 0.f, e = 0.f;
+      float pv[MAXK];
+      for (int c = 0; c < k; ++c) {
+        pv[c] = __expf(to_f(z[c]) - m);
+        s += pv[c];
+        e += pv[c] * bin_value(c, k, lo, hi);
+      }
+      const float x = e / s;
+      const float dx = (float)((c0 + c1 * ((double)x - mx) + c2 * ((double)y - my)) * (double)g);
+      for (int c = 0; c < k; ++c) dz[c] = from_f<T>(dx * (pv[c] / s) * (bin_value(c, k, lo, hi) - x));
+    }
+  }
+}
+
+// ordered stream compaction of (label != ignore) with one block
+__global__ __launch_bounds__(CT) void mask_indices_kernel(int64_t n, const float* label,
+                                                          float ignore, int64_t* idx,
+                                                          int64_t* count) {
+  __shared__ int wsum[CT / 64];
+  __shared__ int64_t base;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t off = 0; off < n; off += CT) {
+    const int64_t i = off + threadIdx.x;
+    const bool keep = i < n && label[i] != ignore;
+    const unsigned long long bal = __ballot(keep);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int wbase = 0;
+    for (int j = 0; j < w; ++j) wbase += wsum[j];
+    if (keep) idx[base + wbase + before] = i;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int j = 0; j < CT / 64; ++j) t += wsum[j];
+      base += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *count = base;
+}
+
+}  // namespace jmt
+
+using namespace jmt;
+
+extern "C" int jmt_ccc_stats(int kind, int pred_dt, int64_t n, int k, const void* pred,
+                             const float* label, float ignore, float lo, float hi, double* stats,
+                             void* stream) {
+  JMT_CHECK_ARG(kind == 0 || kind == 1, "jmt_ccc_stats: kind");
+  JMT_CHECK_ARG(k >= 1 && k <= MAXK, "jmt_ccc_stats: digitize_num %d unsupported", k);
+  JMT_CHECK_ARG(stats && (n == 0 || (pred && label)), "jmt_ccc_stats: null pointer");
+  hipStream_t st = as_stream(stream);
+  switch (pred_dt) {
+    case JMT_F32: hipLaunchKernelGGL((ccc_stats_kernel<float>), dim3(1), dim3(CT), 0, st, kind, n, k, (const float*)pred, label, ignore, lo, hi, stats); break;
+    case JMT_BF16: hipLaunchKernelGGL((ccc_stats_kernel<__bf16>), dim3(1), dim3(CT), 0, st, kind, n, k, (const __bf16*)pred, label, ignore, lo, hi, stats); break;
+    case JMT_F16: hipLaunchKernelGGL((ccc_stats_kernel<_Float16>), dim3(1), dim3(CT), 0, st, kind, n, k, (const _Float16*)pred, label, ignore, lo, hi, stats); break;
+    default: return set_error(JMT_ERR_ARG, "jmt_ccc_stats: dtype");
+  }
+  JMT_LAUNCH_CHECK("jmt_ccc_stats");
+  return JMT_OK;
+}
+
+extern "C" int jmt_ccc_finish(int kind, int world, const double* stats_all, int64_t bs, float eps,
+                              float* loss, double* coef, void* stream) {
+  JMT_CHECK_ARG(world >= 1 && stats_all && loss && coef, "jmt_ccc_finish: bad args");
+  hipLaunchKernelGGL(ccc_finish_kernel, dim3(1), dim3(64), 0, as_stream(stream), kind, world,
+                     stats_all, bs, eps, loss, coef);
+  JMT_LAUNCH_CHECK("jmt_ccc_finish");
+  return JMT_OK;
+}
+
+extern "C" int jmt_ccc_bwd(int kind, int pred_dt, int64_t n, int k, const void* pred,
+                           const float* label, float ignore, float lo, float hi,
+                           const double* coef, const float* grad_loss, void* dpred,
+                           void* stream) {
+  if (n == 0) return JMT_OK;
+  JMT_CHECK_ARG(k >= 1 && k <= MAXK && pred && label && coef && dpred, "jmt_ccc_bwd: bad args");
+  hipStream_t st = as_stream(stream);
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  switch (pred_dt) {
+    case JMT_F32: hipLaunchKernelGGL((ccc_bwd_kernel<float>), dim3(blocks), dim3(256), 0, st, kind, n, k, (const float*)pred, label, ignore, lo, hi, coef, grad_loss, (float*)dpred); break;
+    case JMT_BF16: hipLaunchKernelGGL((ccc_bwd_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, kind, n, k, (const __bf16*)pred, label, ignore, lo, hi, coef, grad_loss, (__bf16*)dpred); break;
+    case JMT_F16: hipLaunchKernelGGL((ccc_bwd_kernel<_Float16>), dim3(blocks), dim3(256), 0, st, kind, n, k, (const _Float16*)pred, label, ignore, lo, hi, coef, grad_loss, (_Float16*)dpred); break;
+    default: return set_error(JMT_ERR_ARG, "jmt_ccc_bwd: dtype");
+  }
+  JMT_LAUNCH_CHECK("jmt_ccc_bwd");
+  return JMT_OK;
+}
+
+extern "C" int jmt_mask_indices(int64_t n, const float* label, float ignore, int64_t* idx,
+                                int64_t* count, void* stream) {
+  JMT_CHECK_ARG(idx && count && (n == 0 || label), "jmt_mask_indices: null pointer");
+  hipLaunchKernelGGL(mask_indices_kernel, dim3(1), dim3(CT), 0, as_stream(stream), n, label,
+                     ignore, idx, count);
+  JMT_LAUNCH_CHECK("jmt_mask_indices");
+  return JMT_OK;
+}

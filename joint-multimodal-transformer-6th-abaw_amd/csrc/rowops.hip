@@ -1,0 +1,402 @@
+// Row-wise / reduction kernels of the JMT path (gfx950, wave64): L2 normalize, residual+LayerNorm,
+// attention softmax, bias-gradient column sums, strided copies.  All HBM-bound: one wave owns a
+// row, lanes stride the row so every wave-instruction is a coalesced 256-B (f32) / 128-B (16-bit)
+// access; statistics in fp32 with two passes (torch's numerics class), cross-row reductions as
+// fp32 partial slabs + a second pass (deterministic, no atomics).
+#include "common.h"
+
+namespace jmt {
+
+constexpr int RB = 256;   // threads per block (4 waves)
+
+template <typename TI>
+__device__ __forceinline__ float ldr(const TI* p, int64_t i) { return to_f(p[i]); }
+
+// ------------------------------------------------------------------ L2 normalize
+template <typename TX, typename TY>
+__global__ __launch_bounds__(RB) void l2norm_fwd_kernel(int64_t rows, int D, const TX* x,
+                                                        int64_t ldx, TY* y, int64_t ldy,
+                                                        float* inv_norm, float eps) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const TX* xr = x + r * ldx;
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const float v = to_f(xr[c]);
+    s += v * v;
+  }
+  s = wave_sum(s);
+  const float inv = 1.f / fmaxf(sqrtf(s), eps);
+  TY* yr = y + r * ldy;
+  for (int c = lane; c < D; c += 64) yr[c] = from_f<TY>(to_f(xr[c]) * inv);
+  if (lane == 0) inv_norm[r] = inv;
+}
+
+template <typename TX, typename TG, typename TD>
+__global__ __launch_bounds__(RB) void l2norm_bwd_kernel(int64_t rows, int D, const TX* x,
+                                                        int64_t ldx, const TG* dy, int64_t lddy,
+                                                        const float* inv_norm, float eps, TD* dx,
+                                                        int64_t lddx) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const TX* xr = x + r * ldx;
+  const TG* gr = dy + r * lddy;
+  const float inv = inv_norm[r];
+  // ||x|| > eps  <=>  inv < 1/eps ; clamp_min's gradient is zero on the clamped side
+  const bool clamped = !(inv < 1.f / eps);
+  float dot = 0.f;
+  for (int c = lane; c < D; c += 64) dot += to_f(xr[c]) * inv * to_f(gr[c]);
+  dot = wave_sum(dot);
+  TD* dr = dx + r * lddx;
+  for (int c = lane; c < D; c += 64) {
+    const float yv = to_f(xr[c]) * inv;
+    const float g = to_f(gr[c]);
+    dr[c] = from_f<TD>(clamped ? g * inv : (g - yv * dot) * inv);
+  }
+}
+
+// ------------------------------------------------------------------ residual + LayerNorm
+template <typename TI, typename TO>
+__global__ __launch_bounds__(RB) void ln_fwd_kernel(int64_t rows, int D, const TI* x, int64_t ldx,
+                                                    const TI* rr, int64_t ldr, const float* gamma,
+                                                    const float* beta, float eps, TO* y,
+                                                    int64_t ldy, float* mean, float* rstd) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const TI* xr = x + r * ldx;
+  const TI* res = rr ? rr + r * ldr : nullptr;
+  constexpr int MAXC = 32;   // D <= 2048
+  float v[MAXC];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + 64 * j;
+    float t = 0.f;
+    if (c < D) {
+      t = to_f(xr[c]);
+      if (res) t += to_f(res[c]);
+    }
+    v[j] = t;
+    s += t;
+  }
+  const float mu = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + 64 * j;
+    if (c < D) {
+      const float d = v[j] - mu;
+      q += d * d;
+    }
+  }
+  const float var = wave_sum(q) / (float)D;
+  const float rs = rsqrtf(var + eps);
+  TO* yr = y + r * ldy;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + 64 * j;
+    if (c < D) yr[c] = from_f<TO>((v[j] - mu) * rs * gamma[c] + beta[c]);
+  }
+  if (lane == 0) {
+    mean[r] = mu;
+    rstd[r] = rs;
+  }
+}
+
+constexpr int LN_ROWS_PER_BLOCK = 64;   // 16 rows per wave
+
+template <typename TI, typename TG, typename TD>
+__global__ __launch_bounds__(RB) void ln_bwd_kernel(int64_t rows, int D, const TI* x, int64_t ldx,
+                                                    const TI* rr, int64_t ldr, const TG* dy,
+                                                    int64_t lddy, const float* mean,
+                                                    const float* rstd, const float* gamma, TD* dx,
+                                                    int64_t lddx, float* partials) {
+  constexpr int MAXC = 32;
+  __shared__ float red[4][2][64];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  float pg[MAXC], pb[MAXC];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) pg[j] = pb[j] = 0.f;
+  const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK;
+  for (int i = w; i < LN_ROWS_PER_BLOCK; i += 4) {
+    const int64_t r = rbeg + i;
+    if (r >= rows) break;
+    const float mu = mean[r], rs = rstd[r];
+    const TI* xr = x + r * ldx;
+    const TI* res = rr ? rr + r * ldr : nullptr;
+    const TG* gr = dy + r * lddy;
+    float xh[MAXC], gd[MAXC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + 64 * j;
+      xh[j] = 0.f;
+      gd[j] = 0.f;
+      if (c < D) {
+        float t = to_f(xr[c]);
+        if (res) t += to_f(res[c]);
+        xh[j] = (t - mu) * rs;
+        const float g = to_f(gr[c]);
+        pg[j] += g * xh[j];
+        pb[j] += g;
+        gd[j] = g * gamma[c];
+        s1 += gd[j];
+        s2 += gd[j] * xh[j];
+      }
+    }
+    s1 = wave_sum(s1) / (float)D;
+    s2 = wave_sum(s2) / (float)D;
+    TD* dr = dx + r * lddx;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + 64 * j;
+      if (c < D) dr[c] = from_f<TD>(rs * (gd[j] - s1 - xh[j] * s2));
+    }
+  }
+  // block-reduce the per-wave column partials -> partials[blk][2][D]
+  float* out = partials + (int64_t)blockIdx.x * 2 * D;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + 64 * j;
+    if (64 * j >= D) break;
+    red[w][0][lane] = pg[j];
+    red[w][1][lane] = pb[j];
+    __syncthreads();
+    if (w == 0 && c < D) {
+      out[c] = red[0][0][lane] + red[1][0][lane] + red[2][0][lane] + red[3][0][lane];
+      out[D + c] = red[0][1][lane] + red[1][1][lane] + red[2][1][lane] + red[3][1][lane];
+    }
+    __syncthreads();
+  }
+}
+
+// sum partial slabs: out[c] (+)= sum_b partials[b*stride + off + c]
+__global__ __launch_bounds__(RB) void slab_reduce_kernel(int nblk, int D, const float* partials,
+                                                         int64_t stride, int64_t off, float* out,
+                                                         int beta_acc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += partials[(int64_t)b * stride + off + c];
+  out[c] = beta_acc ? out[c] + s : s;
+}
+
+// ------------------------------------------------------------------ softmax
+template <typename TP>
+__global__ __launch_bounds__(RB) void softmax_fwd_kernel(int64_t rows, int n, const float* s,
+                                                         int64_t lds, float scale, TP* p,
+                                                         int64_t ldp) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float* sr = s + r * lds;
+  float m = -INFINITY;
+  for (int c = lane; c < n; c += 64) m = fmaxf(m, sr[c] * scale);
+  m = wave_max(m);
+  float z = 0.f;
+  for (int c = lane; c < n; c += 64) z += __expf(sr[c] * scale - m);
+  z = wave_sum(z);
+  const float iz = 1.f / z;
+  TP* pr = p + r * ldp;
+  for (int c = lane; c < ldp; c += 64)
+    pr[c] = from_f<TP>(c < n ? __expf(sr[c] * scale - m) * iz : 0.f);
+}
+
+template <typename TP, typename TS>
+__global__ __launch_bounds__(RB) void softmax_bwd_kernel(int64_t rows, int n, const TP* p,
+                                                         int64_t ldp, const float* dp,
+                                                         int64_t lddp, float scale, TS* ds,
+                                                         int64_t ldds) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const TP* pr = p + r * ldp;
+  const float* gr = dp + r * lddp;
+  float dot = 0.f;
+  for (int c = lane; c < n; c += 64) dot += to_f(pr[c]) * gr[c];
+  dot = wave_sum(dot);
+  TS* dr = ds + r * ldds;
+  for (int c = lane; c < ldds; c += 64)
+    dr[c] = from_f<TS>(c < n ? scale * to_f(pr[c]) * (gr[c] - dot) : 0.f);
+}
+
+// ------------------------------------------------------------------ column sums (bias grad)
+constexpr int CS_ROWS = 128;
+
+template <typename T>
+__global__ __launch_bounds__(RB) void colsum_kernel(int64_t rows, int N, const T* dy, int64_t ld,
+                                                    float* partials) {
+  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.x * CS_ROWS;
+  const int64_t r1 = min(rows, r0 + CS_ROWS);
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += to_f(dy[r * ld + c]);
+  partials[(int64_t)blockIdx.x * N + c] = s;
+}
+
+// ------------------------------------------------------------------ strided copy
+__global__ __launch_bounds__(RB) void copy2d_kernel(int sdt, int ddt, int64_t rows, int64_t cols,
+                                                    const void* src, int64_t srs, int64_t scs,
+                                                    void* dst, int64_t drs, int64_t dcs, int acc) {
+  const int64_t total = rows * cols;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / cols, c = e - r * cols;
+    float v = ld_dyn(src, r * srs + c * scs, sdt);
+    const int64_t o = r * drs + c * dcs;
+    if (acc) v += ld_dyn(dst, o, ddt);
+    st_dyn(dst, o, ddt, v);
+  }
+}
+
+static inline unsigned row_blocks(int64_t rows) { return (unsigned)((rows + 3) / 4); }
+
+}  // namespace jmt
+
+using namespace jmt;
+
+// dtype dispatch helpers --------------------------------------------------------------------
+#define JMT_DISPATCH1(dt, T, ...)                        \
+  switch (dt) {                                          \
+    case JMT_F32: { typedef float T; __VA_ARGS__; } break;     \
+    case JMT_BF16: { typedef __bf16 T; __VA_ARGS__; } break;   \
+    case JMT_F16: { typedef _Float16 T; __VA_ARGS__; } break;  \
+    default: return set_error(JMT_ERR_ARG, "bad dtype %d", (int)dt); \
+  }
+
+extern "C" int jmt_l2norm_fwd(int x_dt, int y_dt, int64_t rows, int D, const void* x, int64_t ldx,
+                              void* y, int64_t ldy, float* inv_norm, float eps, void* stream) {
+  if (rows == 0) return JMT_OK;
+  JMT_CHECK_ARG(D > 0 && x && y && inv_norm, "jmt_l2norm_fwd: bad args");
+  hipStream_t st = as_stream(stream);
+  JMT_DISPATCH1(x_dt, TX, JMT_DISPATCH1(y_dt, TY,
+      hipLaunchKernelGGL((l2norm_fwd_kernel<TX, TY>), dim3(row_blocks(rows)), dim3(RB), 0, st,
+                         rows, D, (const TX*)x, ldx, (TY*)y, ldy, inv_norm, eps)));
+  JMT_LAUNCH_CHECK("jmt_l2norm_fwd");
+  return JMT_OK;
+}
+
+extern "C" int jmt_l2norm_bwd(int x_dt, int dy_dt, int dx_dt, int64_t rows, int D, const void* x,
+                              int64_t ldx, const void* dy, int64_t lddy, const float* inv_norm,
+                              float eps, void* dx, int64_t lddx, void* stream) {
+  if (rows == 0) return JMT_OK;
+  JMT_CHECK_ARG(D > 0 && x && dy && dx && inv_norm, "jmt_l2norm_bwd: bad args");
+  hipStream_t st = as_stream(stream);
+  JMT_DISPATCH1(x_dt, TX, JMT_DISPATCH1(dy_dt, TG, JMT_DISPATCH1(dx_dt, TD,
+      hipLaunchKernelGGL((l2norm_bwd_kernel<TX, TG, TD>), dim3(row_blocks(rows)), dim3(RB), 0, st,
+                         rows, D, (const TX*)x, ldx, (const TG*)dy, lddy, inv_norm, eps, (TD*)dx,
+                         lddx))));
+  JMT_LAUNCH_CHECK("jmt_l2norm_bwd");
+  return JMT_OK;
+}
+
+extern "C" int jmt_layernorm_fwd(int dt_in, int dt_out, int64_t rows, int D, const void* x,
+                                 int64_t ldx, const void* r, int64_t ldr, const float* gamma,
+                                 const float* beta, float eps, void* y, int64_t ldy, float* mean,
+                                 float* rstd, void* stream) {
+  if (rows == 0) return JMT_OK;
+  JMT_CHECK_ARG(D > 0 && D <= 2048, "jmt_layernorm_fwd: D=%d unsupported (<=2048)", D);
+  JMT_CHECK_ARG(x && y && gamma && beta && mean && rstd, "jmt_layernorm_fwd: null pointer");
+  hipStream_t st = as_stream(stream);
+  JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_out, TO,
+      hipLaunchKernelGGL((ln_fwd_kernel<TI, TO>), dim3(row_blocks(rows)), dim3(RB), 0, st, rows, D,
+                         (const TI*)x, ldx, (const TI*)r, ldr, gamma, beta, eps, (TO*)y, ldy, mean,
+                         rstd)));
+  JMT_LAUNCH_CHECK("jmt_layernorm_fwd");
+  return JMT_OK;
+}
+
+extern "C" int jmt_layernorm_bwd_blocks(int64_t rows) {
+  return (int)((rows + LN_ROWS_PER_BLOCK - 1) / LN_ROWS_PER_BLOCK);
+}
+
+extern "C" int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, int D,
+                                 const void* x, int64_t ldx, const void* r, int64_t ldr,
+                                 const void* dy, int64_t lddy, const float* mean,
+                                 const float* rstd, const float* gamma, void* dx, int64_t lddx,
+                                 float* dgamma, float* dbeta, int beta_acc, float* partials,
+                                 void* stream) {
+  if (rows == 0) return JMT_OK;
+  JMT_CHECK_ARG(D > 0 && D <= 2048, "jmt_layernorm_bwd: D=%d unsupported (<=2048)", D);
+  JMT_CHECK_ARG(x && dy && dx && mean && rstd && gamma && partials && dgamma && dbeta,
+                "jmt_layernorm_bwd: null pointer");
+  hipStream_t st = as_stream(stream);
+  const int nblk = jmt_layernorm_bwd_blocks(rows);
+  JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_dy, TG, JMT_DISPATCH1(dt_dx, TD,
+      hipLaunchKernelGGL((ln_bwd_kernel<TI, TG, TD>), dim3(nblk), dim3(RB), 0, st, rows, D,
+                         (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd,
+                         gamma, (TD*)dx, lddx, partials))));
+  JMT_LAUNCH_CHECK("jmt_layernorm_bwd");
+  const unsigned g = (unsigned)((D + RB - 1) / RB);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(g), dim3(RB), 0, st, nblk, D, partials,
+                     (int64_t)2 * D, (int64_t)0, dgamma, beta_acc);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(g), dim3(RB), 0, st, nblk, D, partials,
+                     (int64_t)2 * D, (int64_t)D, dbeta, beta_acc);
+  JMT_LAUNCH_CHECK("jmt_layernorm_bwd(reduce)");
+  return JMT_OK;
+}
+
+extern "C" int jmt_softmax_fwd(int p_dt, int64_t rows, int n, const float* s, int64_t lds,
+                               float scale, void* p, int64_t ldp, void* stream) {
+  if (rows == 0) return JMT_OK;
+  JMT_CHECK_ARG(n > 0 && ldp >= n && s && p, "jmt_softmax_fwd: bad args");
+  hipStream_t st = as_stream(stream);
+  JMT_DISPATCH1(p_dt, TP,
+      hipLaunchKernelGGL((softmax_fwd_kernel<TP>), dim3(row_blocks(rows)), dim3(RB), 0, st, rows,
+                         n, s, lds, scale, (TP*)p, ldp));
+  JMT_LAUNCH_CHECK("jmt_softmax_fwd");
+  return JMT_OK;
+}
+
+extern "C" int jmt_softmax_bwd(int p_dt, int ds_dt, int64_t rows, int n, const void* p,
+                               int64_t ldp, const float* dp, int64_t lddp, float scale, void* ds,
+                               int64_t ldds, void* stream) {
+  if (rows == 0) return JMT_OK;
+  JMT_CHECK_ARG(n > 0 && ldds >= n && p && dp && ds, "jmt_softmax_bwd: bad args");
+  hipStream_t st = as_stream(stream);
+  JMT_DISPATCH1(p_dt, TP, JMT_DISPATCH1(ds_dt, TS,
+      hipLaunchKernelGGL((softmax_bwd_kernel<TP, TS>), dim3(row_blocks(rows)), dim3(RB), 0, st,
+                         rows, n, (const TP*)p, ldp, dp, lddp, scale, (TS*)ds, ldds)));
+  JMT_LAUNCH_CHECK("jmt_softmax_bwd");
+  return JMT_OK;
+}
+
+extern "C" int jmt_colsum_blocks(int64_t rows) { return (int)((rows + CS_ROWS - 1) / CS_ROWS); }
+
+extern "C" int jmt_colsum(int dt, int64_t rows, int N, const void* dy, int64_t ld, float* db,
+                          int beta_acc, float* partials, void* stream) {
+  JMT_CHECK_ARG(N > 0 && db && partials, "jmt_colsum: bad args");
+  hipStream_t st = as_stream(stream);
+  const int nblk = jmt_colsum_blocks(rows);
+  if (nblk == 0) {
+    if (!beta_acc) (void)hipMemsetAsync(db, 0, sizeof(float) * N, st);
+    return JMT_OK;
+  }
+  JMT_DISPATCH1(dt, T,
+      hipLaunchKernelGGL((colsum_kernel<T>), dim3(nblk, (N + RB - 1) / RB), dim3(RB), 0, st, rows,
+                         N, (const T*)dy, ld, partials));
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((N + RB - 1) / RB), dim3(RB), 0, st, nblk, N,
+                     partials, (int64_t)N, (int64_t)0, db, beta_acc);
+  JMT_LAUNCH_CHECK("jmt_colsum");
+  return JMT_OK;
+}
+
+extern "C" int jmt_copy2d(int src_dt, int dst_dt, int64_t rows, int64_t cols, const void* src,
+                          int64_t src_rs, int64_t src_cs, void* dst, int64_t dst_rs,
+                          int64_t dst_cs, int accumulate, void* stream) {
+  if (rows == 0 || cols == 0) return JMT_OK;
+  JMT_CHECK_ARG(src && dst, "jmt_copy2d: null pointer");
+  JMT_CHECK_ARG(src_dt >= 0 && src_dt <= 2 && dst_dt >= 0 && dst_dt <= 2, "jmt_copy2d: dtype");
+  const int64_t total = rows * cols;
+  int blocks = (int)((total + RB - 1) / RB);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(copy2d_kernel, dim3(blocks), dim3(RB), 0, as_stream(stream), src_dt, dst_dt,
+                     rows, cols, src, src_rs, src_cs, dst, dst_rs, dst_cs, accumulate);
+  JMT_LAUNCH_CHECK("jmt_copy2d");
+  return JMT_OK;
+}

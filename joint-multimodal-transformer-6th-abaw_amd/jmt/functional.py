@@ -1,0 +1,651 @@
+"""Autograd functions of the JMT hot path.  Forward and backward of every op are launches of
+libjmt_hip.so kernels (jmt/ops.py); torch supplies device memory, streams and the autograd tape.
+
+Layout conventions
+  * Activations are (rows, features) with the feature axis contiguous.  A logical tensor whose
+    leading axes are a permutation of a dense buffer (the reference's permute(1,0,2) between
+    (B,T,E) and seq-first (T,B,E), mm_multi_transformers.py:127-129) is processed in memory order
+    and results are returned with the same permutation: permutes are free.
+  * Parameters stay fp32 nn.Parameters (state_dict compatible).  In 16-bit compute mode each
+    weight is read through a cached bf16/f16 shadow (re-cast only when the parameter changes).
+  * Parameter gradients are written straight into `param.grad` by the wgrad GEMM / reduction
+    kernels (beta=1 accumulate), so weights used several times (cross_attention_v is called
+    twice, mm_multi_transformers.py:142-167) and slices of the packed in_proj weight need no
+    autograd adds.
+"""
+from __future__ import annotations
+
+import math
+import weakref
+from typing import Optional
+
+import torch
+from torch.autograd import Function
+
+from . import ops
+from ._lib import F32
+
+# ------------------------------------------------------------------------- precision policy
+_policy = {"dtype": None}
+
+
+def set_compute_dtype(dtype: Optional[torch.dtype]):
+    """None = auto (16-bit under torch.autocast, fp32 otherwise); or force fp32 / bf16 / fp16."""
+    assert dtype in (None, torch.float32, torch.bfloat16, torch.float16)
+    _policy["dtype"] = dtype
+
+
+def compute_dtype() -> torch.dtype:
+    if _policy["dtype"] is not None:
+        return _policy["dtype"]
+    if torch.is_autocast_enabled("cuda"):
+        return torch.get_autocast_dtype("cuda")
+    return torch.float32
+
+
+class compute_mode:
+    """`with compute_mode(torch.bfloat16): ...`"""
+
+    def __init__(self, dtype):
+        self.dtype = dtype
+
+    def __enter__(self):
+        self.prev = _policy["dtype"]
+        _policy["dtype"] = self.dtype
+        return self
+
+    def __exit__(self, *a):
+        _policy["dtype"] = self.prev
+
+
+def _vec(dtype: torch.dtype) -> int:
+    return 4 if dtype == torch.float32 else 8
+
+
+# ------------------------------------------------------------------------- weight shadows
+_shadows: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def weight_as(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """fp32 parameter -> contiguous compute-dtype copy (cached by parameter identity+version)."""
+    if w.dtype == dtype:
+        return w if w.is_contiguous() else w.contiguous()
+    ent = _shadows.get(w)
+    if ent is not None and ent[0] == w._version and ent[1] == dtype and ent[2] == w.data_ptr():
+        return ent[3]
+    t = ops.cast(w.detach(), dtype)
+    _shadows[w] = (w._version, dtype, w.data_ptr(), t)
+    return t
+
+
+def register_shadow(w: torch.Tensor, shadow: torch.Tensor):
+    """Used by the fused optimizer, which rewrites `shadow` in the same kernel as `w`."""
+    _shadows[w] = (w._version, shadow.dtype, w.data_ptr(), shadow)
+
+
+def _grad_buffer(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if p is None or not p.requires_grad:
+        return None
+    if p.grad is None:
+        p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
+    return p.grad
+
+
+# ------------------------------------------------------------------------- row layouts
+class Rows:
+    """A logical tensor (..., F) seen as `rows` rows of F contiguous features at row stride `ld`,
+    in memory order (a permutation `perm` of the leading axes)."""
+
+    __slots__ = ("t", "shape", "perm", "rows", "ld", "F")
+
+    def __init__(self, x: torch.Tensor, dtype: Optional[torch.dtype] = None):
+        if dtype is not None and x.dtype != dtype:
+            x = _cast_keep_layout(x, dtype)
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        nd = x.dim()
+        lead = list(range(nd - 1))
+        perm = sorted(lead, key=lambda d: (-x.stride(d), d))
+        dims = [d for d in perm if x.shape[d] != 1]
+        ok = all(x.stride(a) == x.stride(b) * x.shape[b] for a, b in zip(dims[:-1], dims[1:]))
+        ld = x.stride(dims[-1]) if dims else max(x.shape[-1], 1)
+        if not ok or ld < x.shape[-1] or ld % _vec(x.dtype) or x.data_ptr() % 16:
+            x = x.contiguous() if x.data_ptr() % 16 == 0 else x.clone()
+            perm = lead
+            ld = x.shape[-1]
+            dims = [d for d in perm if x.shape[d] != 1]
+        self.t = x
+        self.shape = tuple(x.shape)
+        self.perm = perm
+        r = 1
+        for d in lead:
+            r *= x.shape[d]
+        self.rows = r
+        self.ld = ld
+        self.F = x.shape[-1]
+
+    def like(self, F2: int, dtype: torch.dtype, pad_to: int = 1) -> torch.Tensor:
+        """New tensor, same logical leading shape and axis order, last dim F2 (row stride padded
+        to a multiple of `pad_to`)."""
+        Fm = -(-F2 // pad_to) * pad_to
+        msizes = [self.shape[d] for d in self.perm] + [Fm]
+        y = torch.empty(msizes, dtype=dtype, device=self.t.device)
+        if Fm != F2:
+            y = y[..., :F2]
+        inv = [0] * len(self.perm)
+        for i, d in enumerate(self.perm):
+            inv[d] = i
+        return y.permute(*inv, len(self.perm))
+
+    def same_rows(self, other: "Rows") -> bool:
+        return self.perm == other.perm and self.shape[:-1] == other.shape[:-1]
+
+
+def _cast_keep_layout(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    if x.stride(-1) == 1 and x.is_contiguous():
+        return ops.cast(x, dtype)
+    L = Rows(x)
+    y = L.like(L.F, dtype)
+    ops.copy2d(L.t.data_ptr(), ops.dt(L.t), y.data_ptr(), ops.dt(y), L.rows, L.F, L.ld, 1,
+               _ld(y, L.perm), 1)
+    return y
+
+
+def _ld(y: torch.Tensor, perm) -> int:
+    dims = [d for d in perm if y.shape[d] != 1]
+    return y.stride(dims[-1]) if dims else max(y.shape[-1], 1)
+
+
+def _ptr(t: torch.Tensor, elem_off: int = 0) -> int:
+    return t.data_ptr() + elem_off * t.element_size()
+
+
+def _match(g: torch.Tensor, L: Rows, dtype: torch.dtype) -> Rows:
+    """Bring an incoming gradient to layout L and compute dtype."""
+    G = Rows(g, dtype)
+    if G.same_rows(L):
+        return G
+    y = L.like(L.F if g.shape[-1] == L.F else g.shape[-1], dtype)
+    y.copy_(g)   # rare: autograd handed us a differently laid-out gradient
+    return Rows(y)
+
+
+def _dc(d: torch.dtype) -> int:
+    return ops.dt(d)
+
+
+# ------------------------------------------------------------------------- GEMM helpers
+def _linear_fwd(xin, ld_in, rows, kseg, W, r0, n, b, y, ldy, cd, relu=False):
+    Wc = weight_as(W, cd)
+    nseg = len(xin)
+    ops.gemm(M=rows, N=n, K=kseg * nseg, ab_dtype=_dc(cd), c_dtype=_dc(y.dtype),
+             a=[x.data_ptr() for x in xin], lda=ld_in if rows > 1 else _vec(cd), a_kmajor=True,
+             a_mode=2 if nseg > 1 else 0, a_kseg=kseg if nseg > 1 else 0,
+             b=[_ptr(Wc, r0 * Wc.shape[1])], ldb=Wc.shape[1], b_kmajor=True,
+             c=[y.data_ptr()], ldc=ldy,
+             bias=b[r0:r0 + n] if b is not None else None, bias_mode=1, relu=relu,
+             device=y.device)
+
+
+def _dgrad(G: Rows, n, W, r0, cd, outs, ld_out, nseg, kseg, aux=None, ldaux=0):
+    """outs[s] = (dY . W[r0:r0+n, s*kseg:(s+1)*kseg]) (masked by aux > 0)."""
+    Wc = weight_as(W, cd)
+    Kin = Wc.shape[1]
+    if n == 1:   # dY is a column: read it as an MN-major operand (row stride irrelevant)
+        a_ld, a_kmaj = _vec(cd), False
+    else:
+        a_ld, a_kmaj = G.ld, True
+    ops.gemm(M=G.rows, N=kseg, K=n, ab_dtype=_dc(cd), c_dtype=_dc(outs[0].dtype),
+             a=[G.t.data_ptr()], lda=a_ld, a_kmajor=a_kmaj,
+             b=[_ptr(Wc, r0 * Kin)], ldb=Kin, b_kmajor=False,
+             c=[o.data_ptr() for o in outs], ldc=ld_out, c_mode=1 if nseg > 1 else 0,
+             batch0=nseg, sA=(0, 0), sB=(kseg, 0), sC=(0, 0),
+             aux=aux, ldaux=ldaux, device=G.t.device)
+
+
+def _wgrad(G: Rows, n, xin, ld_in, kseg, W, r0, cd):
+    """W.grad[r0:r0+n, s*kseg:...] += dY^T X_s   (split-K over the rows)."""
+    gW = _grad_buffer(W)
+    if gW is None:
+        return
+    nseg = len(xin)
+    Kin = W.shape[1]
+    # A = dY^T (MN-major); for n == 1 the single row is the contiguous dY column (K-major)
+    a_ld, a_kmaj = (G.ld, False) if n > 1 else (_vec(cd), True)
+    ops.gemm(M=n, N=kseg, K=G.rows, ab_dtype=_dc(cd), c_dtype=F32,
+             a=[G.t.data_ptr()], lda=a_ld, a_kmajor=a_kmaj,
+             b=[x.data_ptr() for x in xin], ldb=ld_in, b_kmajor=False,
+             b_mode=1 if nseg > 1 else 0,
+             c=[_ptr(gW, r0 * Kin)], ldc=Kin, batch0=nseg, sA=(0, 0), sB=(0, 0),
+             sC=(kseg, 0), beta=1.0, device=G.t.device)
+
+
+def _bgrad(G: Rows, n, b, r0):
+    gb = _grad_buffer(b)
+    if gb is not None:
+        ops.colsum(G.t, G.ld, G.rows, n, gb[r0:r0 + n], beta_acc=True)
+
+
+# ------------------------------------------------------------------------- Linear
+class LinearFn(Function):
+    """y = cat(xs, -1) @ W[r0:r0+n]^T + b[r0:r0+n]
+
+    nn.Linear (fc_layer.py:6-12, two_transformers.py:56, mm_multi_transformers.py:99,102,
+    mm_transformers.py:117) and the packed in_proj slices / out_proj of nn.MultiheadAttention.
+    Several `xs` are K-concatenated inside the GEMM without a copy (the torch.cat of
+    mm_multi_transformers.py:120-124, 201-211; mm_transformers.py:140-144; FeatureConcatFC)."""
+
+    @staticmethod
+    def forward(ctx, W, b, r0, n, out_dtype, *xs):
+        cd = compute_dtype()
+        lay = [Rows(x, cd) for x in xs]
+        L0 = lay[0]
+        for l in lay[1:]:
+            if not l.same_rows(L0) or l.ld != L0.ld or l.F != L0.F:
+                raise RuntimeError("LinearFn: concatenated inputs must share one row layout")
+        kseg = L0.F
+        if len(lay) > 1 and kseg % (32 if cd == torch.float32 else 64):
+            raise RuntimeError("LinearFn: concat segment width must be a multiple of 64")
+        odt = out_dtype if out_dtype is not None else cd
+        y = L0.like(n, odt)
+        xin = [l.t for l in lay]
+        _linear_fwd(xin, L0.ld, L0.rows, kseg, W, r0, n, b, y, _ld(y, L0.perm), cd)
+        ctx.save_for_backward(W, b, *xin)
+        ctx.meta = (r0, n, cd, L0, kseg, [x.dtype for x in xs])
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        W, b = ctx.saved_tensors[:2]
+        xin = ctx.saved_tensors[2:]
+        r0, n, cd, L0, kseg, in_dtypes = ctx.meta
+        Gy = _match(gy, Rows(L0.like(n, cd)), cd)
+        nseg = len(xin)
+        dxs = [None] * nseg
+        need = [ctx.needs_input_grad[5 + i] for i in range(nseg)]
+        if any(need):
+            outs = [L0.like(kseg, cd) for _ in range(nseg)]
+            _dgrad(Gy, n, W, r0, cd, outs, _ld(outs[0], L0.perm), nseg, kseg)
+            for i in range(nseg):
+                if need[i]:
+                    dxs[i] = outs[i] if in_dtypes[i] == cd else _cast_keep_layout(outs[i],
+                                                                                  in_dtypes[i])
+        _wgrad(Gy, n, xin, L0.ld, kseg, W, r0, cd)
+        _bgrad(Gy, n, b, r0)
+        return (None, None, None, None, None, *dxs)
+
+
+def linear(xs, W, b=None, r0=0, n=None, out_dtype=None):
+    if isinstance(xs, torch.Tensor):
+        xs = (xs,)
+    if n is None:
+        n = W.shape[0]
+    return LinearFn.apply(W, b, r0, n, out_dtype, *xs)
+
+
+# ------------------------------------------------------------------------- MLP
+class MLPFn(Function):
+    """y = relu(x W1^T + b1) W2^T + b2, ReLU fused into the first GEMM's epilogue and its
+    backward mask fused into the second GEMM's dgrad epilogue.  The transformer feed-forward
+    (mm_multi_transformers.py:52-56) and the V/A regressors with dropout p=0
+    (two_transformers.py:104-114)."""
+
+    @staticmethod
+    def forward(ctx, W1, b1, W2, b2, out_dtype, x):
+        cd = compute_dtype()
+        L = Rows(x, cd)
+        hid, nout = W1.shape[0], W2.shape[0]
+        h = L.like(hid, cd)
+        ldh = _ld(h, L.perm)
+        _linear_fwd([L.t], L.ld, L.rows, L.F, W1, 0, hid, b1, h, ldh, cd, relu=True)
+        odt = out_dtype if out_dtype is not None else cd
+        y = L.like(nout, odt)
+        _linear_fwd([h], ldh, L.rows, hid, W2, 0, nout, b2, y, _ld(y, L.perm), cd)
+        ctx.save_for_backward(W1, b1, W2, b2, L.t, h)
+        ctx.meta = (cd, L, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        W1, b1, W2, b2, xin, h = ctx.saved_tensors
+        cd, L, xdt = ctx.meta
+        hid, nout = W1.shape[0], W2.shape[0]
+        Gy = _match(gy, Rows(L.like(nout, cd)), cd)
+        H = Rows(h)
+        dh = L.like(hid, cd)
+        ldh = _ld(dh, L.perm)
+        _dgrad(Gy, nout, W2, 0, cd, [dh], ldh, 1, hid, aux=h, ldaux=H.ld)
+        _wgrad(Gy, nout, [h], H.ld, hid, W2, 0, cd)
+        _bgrad(Gy, nout, b2, 0)
+        Gh = Rows(dh)
+        dx = None
+        if ctx.needs_input_grad[5]:
+            dx = L.like(L.F, cd)
+            _dgrad(Gh, hid, W1, 0, cd, [dx], _ld(dx, L.perm), 1, L.F)
+            if xdt != cd:
+                dx = _cast_keep_layout(dx, xdt)
+        _wgrad(Gh, hid, [xin], L.ld, L.F, W1, 0, cd)
+        _bgrad(Gh, hid, b1, 0)
+        return None, None, None, None, None, dx
+
+
+def mlp(x, W1, b1, W2, b2, out_dtype=None):
+    return MLPFn.apply(W1, b1, W2, b2, out_dtype, x)
+
+
+# ------------------------------------------------------------------------- L2 normalize
+class L2NormFn(Function):
+    """F.normalize(x, p=2, dim=-1, eps=1e-12) (two_transformers.py:118-119)."""
+
+    @staticmethod
+    def forward(ctx, x, eps):
+        cd = compute_dtype()
+        L = Rows(x)
+        y = L.like(L.F, cd)
+        inv = torch.empty(L.rows, dtype=torch.float32, device=x.device)
+        ops.l2norm_fwd(L.t, L.ld, L.rows, L.F, y, _ld(y, L.perm), inv, eps)
+        ctx.save_for_backward(L.t, inv)
+        ctx.meta = (L, eps, cd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, inv = ctx.saved_tensors
+        L, eps, cd = ctx.meta
+        G = _match(gy, Rows(L.like(L.F, cd)), cd)
+        dx = L.like(L.F, x.dtype)
+        ops.l2norm_bwd(x, L.ld, G.t, G.ld, inv, eps, dx, _ld(dx, L.perm), L.rows, L.F)
+        return dx, None
+
+
+def l2_normalize(x, eps=1e-12):
+    return L2NormFn.apply(x, eps)
+
+
+# ------------------------------------------------------------------------- residual LayerNorm
+class AddLayerNormFn(Function):
+    """y = LayerNorm(x + r) (mm_multi_transformers.py:64-70: x = layer_norm(x + sublayer(x)))."""
+
+    @staticmethod
+    def forward(ctx, x, r, gamma, beta, eps):
+        cd = compute_dtype()
+        L = Rows(x, cd)
+        R = Rows(r, cd) if r is not None else None
+        if R is not None and not R.same_rows(L):
+            rr = L.like(L.F, cd)
+            rr.copy_(r)
+            R = Rows(rr)
+        y = L.like(L.F, cd)
+        mean = torch.empty(L.rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        ops.layernorm_fwd(L.t, L.ld, R.t if R else None, R.ld if R else 0, gamma, beta, eps, y,
+                          _ld(y, L.perm), mean, rstd, L.rows, L.F)
+        ctx.save_for_backward(L.t, R.t if R else None, gamma, beta, mean, rstd)
+        ctx.meta = (L, R.ld if R else 0, cd, x.dtype, r.dtype if r is not None else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, r, gamma, beta, mean, rstd = ctx.saved_tensors
+        L, ldr, cd, xdt, rdt = ctx.meta
+        G = _match(gy, Rows(L.like(L.F, cd)), cd)
+        dx = L.like(L.F, cd)
+        dg = _grad_buffer(gamma)
+        db = _grad_buffer(beta)
+        tmp = None
+        if dg is None or db is None:
+            tmp = torch.empty(2, L.F, dtype=torch.float32, device=x.device)
+        ops.layernorm_bwd(x, L.ld, r, ldr, G.t, G.ld, mean, rstd, gamma, dx, _ld(dx, L.perm),
+                          dg if dg is not None else tmp[0], db if db is not None else tmp[1],
+                          True if tmp is None else False, L.rows, L.F)
+        dxx = dx if xdt == cd else _cast_keep_layout(dx, xdt)
+        drr = None
+        if r is not None:
+            drr = dx if rdt == cd else _cast_keep_layout(dx, rdt)
+        return dxx, drr, None, None, None
+
+
+def add_layer_norm(x, r, gamma, beta, eps=1e-5):
+    return AddLayerNormFn.apply(x, r, gamma, beta, eps)
+
+
+# ------------------------------------------------------------------------- attention core
+def _round_up(a, b):
+    return -(-a // b) * b
+
+
+class AttnCoreFn(Function):
+    """softmax(Q K^T / sqrt(dh)) V per (batch, head) — the core of F.multi_head_attention_forward
+    (SURVEY.md §8a a6).  Q/K/V are column slices (qcol/kcol/vcol) of the in-projection outputs
+    q_src (Lq, N, *), k_src / v_src (Lk, N, *) in any strided seq-first layout, so self-attention
+    (one packed qkv) and key-is-value cross-attention (q + packed kv) read their projections in
+    place and write their gradients into packed buffers consumed by ONE in_proj dgrad/wgrad.
+    Scores are materialised as fp32 (N, H, Lq, ldS), probabilities in the compute dtype."""
+
+    @staticmethod
+    def forward(ctx, q_src, k_src, v_src, E, H, qcol, kcol, vcol):
+        cd = compute_dtype()
+        for t in (q_src, k_src, v_src):
+            assert t.dtype == cd and t.stride(-1) == 1
+        Lq, N = q_src.shape[0], q_src.shape[1]
+        Lk = k_src.shape[0]
+        dh = E // H
+        dev = q_src.device
+        sq_l, sq_n = q_src.stride(0), q_src.stride(1)
+        sk_l, sk_n = k_src.stride(0), k_src.stride(1)
+        sv_l, sv_n = v_src.stride(0), v_src.stride(1)
+        ldS = _round_up(Lk, 8)
+        bS = (H * Lq * ldS, Lq * ldS)
+        S = torch.empty(N * H * Lq * ldS, dtype=torch.float32, device=dev)
+        ops.gemm(M=Lq, N=Lk, K=dh, ab_dtype=_dc(cd), c_dtype=F32,
+                 a=[_ptr(q_src, qcol)], lda=sq_l, a_kmajor=True, sA=(sq_n, dh),
+                 b=[_ptr(k_src, kcol)], ldb=sk_l, b_kmajor=True, sB=(sk_n, dh),
+                 c=[S.data_ptr()], ldc=ldS, sC=bS, batch0=N, batch1=H, device=dev)
+        P = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
+        scale = 1.0 / math.sqrt(dh)
+        ops.softmax_fwd(S, ldS, N * H * Lq, Lk, scale, P, ldS)
+        del S
+        o = Rows(q_src).like(E, cd)
+        ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                 a=[P.data_ptr()], lda=ldS, a_kmajor=True, sA=bS,
+                 b=[_ptr(v_src, vcol)], ldb=sv_l, b_kmajor=False, sB=(sv_n, dh),
+                 c=[o.data_ptr()], ldc=o.stride(0), sC=(o.stride(1), dh),
+                 batch0=N, batch1=H, device=dev)
+        ctx.save_for_backward(q_src, k_src, v_src, P)
+        # which inputs are the same tensor (saved tensors are not guaranteed to unpack to the
+        # same Python objects, so the aliasing is recorded here)
+        owner = (0, 0 if k_src is q_src else 1,
+                 0 if v_src is q_src else (1 if v_src is k_src else 2))
+        ctx.meta = (E, H, qcol, kcol, vcol, ldS, scale, cd, owner)
+        return o
+
+    @staticmethod
+    def backward(ctx, go):
+        q_src, k_src, v_src, P = ctx.saved_tensors
+        E, H, qcol, kcol, vcol, ldS, scale, cd, owner = ctx.meta
+        Lq, N = q_src.shape[0], q_src.shape[1]
+        Lk = k_src.shape[0]
+        dh = E // H
+        dev = q_src.device
+        v8 = _vec(cd)
+        if go.dtype != cd or go.stride(-1) != 1 or go.stride(0) % v8 or go.stride(1) % v8:
+            go = _cast_keep_layout(go if go.stride(-1) == 1 else go.contiguous(), cd)
+        sq_l, sq_n = q_src.stride(0), q_src.stride(1)
+        sk_l, sk_n = k_src.stride(0), k_src.stride(1)
+        sv_l, sv_n = v_src.stride(0), v_src.stride(1)
+        so_l, so_n = go.stride(0), go.stride(1)
+        bS = (H * Lq * ldS, Lq * ldS)
+        dP = torch.empty(N * H * Lq * ldS, dtype=torch.float32, device=dev)
+        ops.gemm(M=Lq, N=Lk, K=dh, ab_dtype=_dc(cd), c_dtype=F32,
+                 a=[go.data_ptr()], lda=so_l, a_kmajor=True, sA=(so_n, dh),
+                 b=[_ptr(v_src, vcol)], ldb=sv_l, b_kmajor=True, sB=(sv_n, dh),
+                 c=[dP.data_ptr()], ldc=ldS, sC=bS, batch0=N, batch1=H, device=dev)
+        dS = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
+        ops.softmax_bwd(P, ldS, dP, ldS, N * H * Lq, Lk, scale, dS, ldS)
+        del dP
+        # one gradient buffer per distinct source tensor (packed qkv -> one buffer)
+        srcs = (q_src, k_src, v_src)
+        bufs = [None, None, None]
+        for i in range(3):
+            if owner[i] == i:
+                bufs[i] = Rows(srcs[i]).like(srcs[i].shape[-1], cd)
+        dq, dk, dv = bufs[owner[0]], bufs[owner[1]], bufs[owner[2]]
+        # dQ = dS K
+        ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                 a=[dS.data_ptr()], lda=ldS, a_kmajor=True, sA=bS,
+                 b=[_ptr(k_src, kcol)], ldb=sk_l, b_kmajor=False, sB=(sk_n, dh),
+                 c=[_ptr(dq, qcol)], ldc=dq.stride(0), sC=(dq.stride(1), dh), batch0=N,
+                 batch1=H, device=dev)
+        # dK = dS^T Q
+        ops.gemm(M=Lk, N=dh, K=Lq, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                 a=[dS.data_ptr()], lda=ldS, a_kmajor=False, sA=bS,
+                 b=[_ptr(q_src, qcol)], ldb=sq_l, b_kmajor=False, sB=(sq_n, dh),
+                 c=[_ptr(dk, kcol)], ldc=dk.stride(0), sC=(dk.stride(1), dh), batch0=N,
+                 batch1=H, device=dev)
+        # dV = P^T dO
+        ops.gemm(M=Lk, N=dh, K=Lq, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                 a=[P.data_ptr()], lda=ldS, a_kmajor=False, sA=bS,
+                 b=[go.data_ptr()], ldb=so_l, b_kmajor=False, sB=(so_n, dh),
+                 c=[_ptr(dv, vcol)], ldc=dv.stride(0), sC=(dv.stride(1), dh), batch0=N,
+                 batch1=H, device=dev)
+        grads = [bufs[i] if owner[i] == i else None for i in range(3)]
+        return (*grads, None, None, None, None, None)
+
+
+def multihead_attention(query, key, value, in_w, in_b, out_w, out_b, num_heads):
+    """nn.MultiheadAttention(E, H)(query, key, value) with dropout 0, seq-first (L, N, E).
+    Every reference call site passes key is value: then K and V come from
+    one packed in_proj GEMM (and Q too for self-attention)."""
+    E = in_w.shape[1]
+    if query is key and key is value:
+        qkv = linear(query, in_w, in_b, 0, 3 * E)
+        o = AttnCoreFn.apply(qkv, qkv, qkv, E, num_heads, 0, E, 2 * E)
+    elif key is value:
+        q = linear(query, in_w, in_b, 0, E)
+        kv = linear(key, in_w, in_b, E, 2 * E)
+        o = AttnCoreFn.apply(q, kv, kv, E, num_heads, 0, 0, E)
+    else:
+        q = linear(query, in_w, in_b, 0, E)
+        k = linear(key, in_w, in_b, E, E)
+        v = linear(value, in_w, in_b, 2 * E, E)
+        o = AttnCoreFn.apply(q, k, v, E, num_heads, 0, 0, 0)
+    return linear(o, out_w, out_b)
+
+
+# ------------------------------------------------------------------------- stack / transpose
+class StackSeqFn(Function):
+    """torch.stack(xs, dim=2) of seq-first (T, B, E) tensors followed by permute(1,0,2,3),
+    flatten(0,1), permute(1,0,2) (mm_multi_transformers.py:171-178) — or of batch-first (B,T,E)
+    tensors followed by flatten(0,1).permute(1,0,2) (intra_modal_transformer_fusion.py:93-97):
+    returns the seq-first (S, B*T, E) view of one (B, T, S, E) buffer filled by strided copies.
+    The backward hands out strided views of the incoming gradient (no copies)."""
+
+    @staticmethod
+    def forward(ctx, seq_first_in, *xs):
+        cd = compute_dtype()
+        S = len(xs)
+        x0 = xs[0]
+        if seq_first_in:
+            T, B, E = x0.shape
+        else:
+            B, T, E = x0.shape
+        buf = torch.empty(B, T, S, E, dtype=cd, device=x0.device)
+        for s, x in enumerate(xs):
+            xb = x.permute(1, 0, 2) if seq_first_in else x      # (B, T, E) logical
+            if xb.stride(2) == 1 and xb.stride(0) == T * xb.stride(1):
+                ops.copy2d(xb.data_ptr(), ops.dt(xb), _ptr(buf, s * E), ops.dt(buf), B * T, E,
+                           xb.stride(1), 1, S * E, 1)
+            else:
+                for bi in range(B):
+                    xr = xb[bi]
+                    ops.copy2d(xr.data_ptr(), ops.dt(xr), _ptr(buf, (bi * T * S + s) * E),
+                               ops.dt(buf), T, E, xr.stride(0), xr.stride(1), S * E, 1)
+        ctx.meta = (S, seq_first_in, B, T, E)
+        return buf.view(B * T, S, E).permute(1, 0, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        S, seq_first_in, B, T, E = ctx.meta
+        gb = g.permute(1, 0, 2)
+        gb = gb.view(B, T, S, E) if gb.is_contiguous() else gb.reshape(B, T, S, E)
+        res = [gb[:, :, s, :].permute(1, 0, 2) if seq_first_in else gb[:, :, s, :]
+               for s in range(S)]
+        return (None, *res)
+
+
+def stack_seq(xs, seq_first_in=True):
+    return StackSeqFn.apply(seq_first_in, *xs)
+
+
+class TransposeCopyFn(Function):
+    """Contiguous copy of a 2-D (T, B) view (the seq-first V/A predictions of the FC head,
+    two_transformers.py:125-128) so that train.py:303-307's .view(-1, T*B) works."""
+
+    @staticmethod
+    def forward(ctx, x):
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        ops.copy2d(x.data_ptr(), ops.dt(x), out.data_ptr(), ops.dt(out), x.shape[0], x.shape[1],
+                   x.stride(0), x.stride(1), x.shape[1], 1)
+        ctx.meta = (x.shape, x.stride(), x.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        shape, stride, dtype = ctx.meta
+        base = torch.empty_strided(shape, stride, dtype=g.dtype, device=g.device)
+        ops.copy2d(g.data_ptr(), ops.dt(g), base.data_ptr(), ops.dt(base), shape[0], shape[1],
+                   g.stride(0), g.stride(1), base.stride(0), base.stride(1))
+        return base
+
+
+# ------------------------------------------------------------------------- CCC losses
+class CCCLossFn(Function):
+    """losses/loss.py:18-32 (kind 0) and losses/CCCLoss.py:15-43 (kind 1) as one statistics
+    kernel + (optional) all-gather of 8 doubles per rank + one finish kernel; backward is one
+    elementwise kernel.  With a process group the loss is the GLOBAL-batch CCC, exactly what the
+    reference computes after its DataParallel gather."""
+
+    @staticmethod
+    def forward(ctx, pred, label, kind, k, ignore, lo, hi, eps, bs, group):
+        dev = pred.device
+        pred_c = pred if pred.is_contiguous() else pred.contiguous()
+        lab = label
+        if lab.dtype != torch.float32 or not lab.is_contiguous():
+            lab = ops.cast(lab, torch.float32)
+        stats = torch.empty(8, dtype=torch.float64, device=dev)
+        ops.ccc_stats(kind, pred_c, lab, k, ignore, lo, hi, stats)
+        world = 1
+        stats_all = stats
+        if group is not None:
+            import torch.distributed as dist
+            world = dist.get_world_size(group)
+            if world > 1:
+                stats_all = torch.empty(8 * world, dtype=torch.float64, device=dev)
+                dist.all_gather_into_tensor(stats_all, stats, group=group)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        coef = torch.empty(8, dtype=torch.float64, device=dev)
+        ops.ccc_finish(kind, world, stats_all, bs, eps, loss, coef)
+        ctx.save_for_backward(pred_c, lab, coef)
+        ctx.meta = (kind, k, ignore, lo, hi, pred.shape)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, lab, coef = ctx.saved_tensors
+        kind, k, ignore, lo, hi, shape = ctx.meta
+        g = g.to(torch.float32) if g.dtype != torch.float32 else g
+        g = g.contiguous()
+        dpred = torch.empty_like(pred)
+        ops.ccc_bwd(kind, pred, lab, k, ignore, lo, hi, coef, g, dpred)
+        return dpred.view(shape), None, None, None, None, None, None, None, None, None
+
+
+def ccc_loss(pred, label, eps=1e-8, digitize_num=1, rng=(-1.0, 1.0), group=None):
+    k = int(digitize_num)
+    return CCCLossFn.apply(pred, label, 0, k, 0.0, float(rng[0]), float(rng[1]), float(eps), 1,
+                           group)
+
+
+def ccc_loss_ignore(pred, label, ignore=-5.0, group=None):
+    bs = pred.shape[0]
+    return CCCLossFn.apply(pred, label, 1, 1, float(ignore), -1.0, 1.0, 0.0, int(bs), group)

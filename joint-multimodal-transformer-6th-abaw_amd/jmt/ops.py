@@ -1,0 +1,198 @@
+"""Thin, typed wrappers over the C-ABI: torch tensors in, kernel launches on the current HIP
+stream out.  No math happens here — every op is one (or a few) libjmt_hip.so launches."""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import BF16, F16, F32, GemmDesc
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: F16}
+
+
+def dt(t_or_dtype) -> int:
+    d = t_or_dtype if isinstance(t_or_dtype, torch.dtype) else t_or_dtype.dtype
+    try:
+        return _DT[d]
+    except KeyError:
+        raise _lib.JMTError(f"unsupported dtype {d}") from None
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _require_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.JMTError("JMT HIP ops need device tensors (there is no CPU path)")
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# ------------------------------------------------------------------------------------ GEMM
+
+def auto_splits(M: int, N: int, K: int, batch: int, bk: int = 64) -> int:
+    tiles = math.ceil(M / 128) * math.ceil(N / 128) * batch
+    if tiles >= 192 or K < 4 * bk:
+        return 1
+    want = math.ceil(512 / tiles)
+    return max(1, min(want, K // (2 * bk), 32))
+
+
+def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
+         a: Sequence[int], lda: int, a_kmajor: bool,
+         b: Sequence[int], ldb: int, b_kmajor: bool,
+         c: Sequence[int], ldc: int,
+         a_mode: int = 0, b_mode: int = 0, c_mode: int = 0, a_kseg: int = 0, b_kseg: int = 0,
+         batch0: int = 1, batch1: int = 1, sA=(0, 0), sB=(0, 0), sC=(0, 0),
+         alpha: float = 1.0, beta: float = 0.0, bias: Optional[torch.Tensor] = None,
+         bias_mode: int = 1, relu: bool = False, aux: Optional[torch.Tensor] = None,
+         ldaux: int = 0, splits: Optional[int] = None, device=None) -> None:
+    d = GemmDesc()
+    d.ab_dtype, d.c_dtype = ab_dtype, c_dtype
+    d.aux_dtype = dt(aux) if aux is not None else c_dtype
+    d.M, d.N, d.K = M, N, K
+    for i, p in enumerate(a):
+        d.a[i] = p
+    for i, p in enumerate(b):
+        d.b[i] = p
+    for i, p in enumerate(c):
+        d.c[i] = p
+    d.n_a, d.n_b, d.n_c = len(a), len(b), len(c)
+    d.a_mode, d.b_mode, d.c_mode = a_mode, b_mode, c_mode
+    d.a_kseg, d.b_kseg = a_kseg, b_kseg
+    d.a_kmajor, d.b_kmajor = int(a_kmajor), int(b_kmajor)
+    d.lda, d.ldb, d.ldc, d.ldaux = lda, ldb, ldc, ldaux
+    d.batch0, d.batch1 = batch0, batch1
+    d.sA0, d.sA1 = sA
+    d.sB0, d.sB1 = sB
+    d.sC0, d.sC1 = sC
+    d.alpha, d.beta = alpha, beta
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.bias_mode = bias_mode if bias is not None else 0
+    d.relu = int(relu)
+    d.aux = aux.data_ptr() if aux is not None else None
+    if splits is None:
+        splits = auto_splits(M, N, K, batch0 * batch1, 32 if ab_dtype == F32 else 64)
+    d.splits = splits
+    ws = None
+    if splits > 1:
+        nbytes = _lib.load().jmt_gemm_workspace_bytes(M, N, batch0 * batch1, splits)
+        ws = workspace(nbytes, device)
+        d.workspace = ws.data_ptr()
+        d.ws_bytes = nbytes
+    _lib.check(_lib.load().jmt_gemm(C.byref(d), stream()), "jmt_gemm")
+    return ws   # keep alive until the launch is ordered (caching allocator is stream-ordered)
+
+
+# ------------------------------------------------------------------------------------ rows
+
+def l2norm_fwd(x2: torch.Tensor, ldx: int, rows: int, D: int, y2: torch.Tensor, ldy: int,
+               inv_norm: torch.Tensor, eps: float):
+    _require_cuda(x2, y2)
+    _lib.call("jmt_l2norm_fwd", dt(x2), dt(y2), rows, D, x2.data_ptr(), ldx, y2.data_ptr(), ldy,
+              inv_norm.data_ptr(), eps, stream())
+
+
+def l2norm_bwd(x2, ldx, dy2, lddy, inv_norm, eps, dx2, lddx, rows, D):
+    _lib.call("jmt_l2norm_bwd", dt(x2), dt(dy2), dt(dx2), rows, D, x2.data_ptr(), ldx,
+              dy2.data_ptr(), lddy, inv_norm.data_ptr(), eps, dx2.data_ptr(), lddx, stream())
+
+
+def layernorm_fwd(x, ldx, r, ldr, gamma, beta, eps, y, ldy, mean, rstd, rows, D):
+    _lib.call("jmt_layernorm_fwd", dt(x), dt(y), rows, D, x.data_ptr(), ldx,
+              r.data_ptr() if r is not None else None, ldr, gamma.data_ptr(), beta.data_ptr(),
+              eps, y.data_ptr(), ldy, mean.data_ptr(), rstd.data_ptr(), stream())
+
+
+def layernorm_bwd(x, ldx, r, ldr, dy, lddy, mean, rstd, gamma, dx, lddx, dgamma, dbeta,
+                  beta_acc, rows, D):
+    nblk = _lib.load().jmt_layernorm_bwd_blocks(rows)
+    part = torch.empty(max(nblk, 1) * 2 * D, dtype=torch.float32, device=x.device)
+    _lib.call("jmt_layernorm_bwd", dt(x), dt(dy), dt(dx), rows, D, x.data_ptr(), ldx,
+              r.data_ptr() if r is not None else None, ldr, dy.data_ptr(), lddy,
+              mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), dx.data_ptr(), lddx,
+              dgamma.data_ptr(), dbeta.data_ptr(), int(beta_acc), part.data_ptr(), stream())
+    return part
+
+
+def softmax_fwd(s, lds, rows, n, scale, p, ldp):
+    _lib.call("jmt_softmax_fwd", dt(p), rows, n, s.data_ptr(), lds, scale, p.data_ptr(), ldp,
+              stream())
+
+
+def softmax_bwd(p, ldp, dp, lddp, rows, n, scale, ds, ldds):
+    _lib.call("jmt_softmax_bwd", dt(p), dt(ds), rows, n, p.data_ptr(), ldp, dp.data_ptr(), lddp,
+              scale, ds.data_ptr(), ldds, stream())
+
+
+def colsum(dy, ld, rows, N, db, beta_acc=False):
+    nblk = _lib.load().jmt_colsum_blocks(rows)
+    part = torch.empty(max(nblk, 1) * N, dtype=torch.float32, device=dy.device)
+    _lib.call("jmt_colsum", dt(dy), rows, N, dy.data_ptr(), ld, db.data_ptr(), int(beta_acc),
+              part.data_ptr(), stream())
+    return part
+
+
+def copy2d(src_ptr, src_dt, dst_ptr, dst_dt, rows, cols, src_rs, src_cs, dst_rs, dst_cs,
+           accumulate=False):
+    _lib.call("jmt_copy2d", src_dt, dst_dt, rows, cols, src_ptr, src_rs, src_cs, dst_ptr, dst_rs,
+              dst_cs, int(accumulate), stream())
+
+
+def cast(src: torch.Tensor, dtype: torch.dtype, out: Optional[torch.Tensor] = None):
+    """Contiguous dtype conversion through jmt_copy2d (weight shadows, label upcasts)."""
+    _require_cuda(src)
+    src = src if src.is_contiguous() else src.contiguous()
+    if out is None:
+        out = torch.empty(src.shape, dtype=dtype, device=src.device)
+    n = src.numel()
+    copy2d(src.data_ptr(), dt(src), out.data_ptr(), dt(out), 1, n, n, 1, n, 1)
+    return out
+
+
+# ------------------------------------------------------------------------------------ CCC
+
+def ccc_stats(kind, pred, label, k, ignore, lo, hi, stats):
+    n = label.numel()
+    _lib.call("jmt_ccc_stats", kind, dt(pred), n, k, pred.data_ptr(), label.data_ptr(), ignore,
+              lo, hi, stats.data_ptr(), stream())
+
+
+def ccc_finish(kind, world, stats_all, bs, eps, loss, coef):
+    _lib.call("jmt_ccc_finish", kind, world, stats_all.data_ptr(), bs, eps, loss.data_ptr(),
+              coef.data_ptr(), stream())
+
+
+def ccc_bwd(kind, pred, label, k, ignore, lo, hi, coef, grad_loss, dpred):
+    n = label.numel()
+    _lib.call("jmt_ccc_bwd", kind, dt(pred), n, k, pred.data_ptr(), label.data_ptr(), ignore, lo,
+              hi, coef.data_ptr(), grad_loss.data_ptr() if grad_loss is not None else None,
+              dpred.data_ptr(), stream())
+
+
+def mask_indices(label: torch.Tensor, ignore: float):
+    n = label.numel()
+    idx = torch.empty(max(n, 1), dtype=torch.int64, device=label.device)
+    cnt = torch.empty(1, dtype=torch.int64, device=label.device)
+    _lib.call("jmt_mask_indices", n, label.data_ptr(), ignore, idx.data_ptr(), cnt.data_ptr(),
+              stream())
+    return idx, cnt
+
+
+# ------------------------------------------------------------------------------------ SGD
+
+def sgd_step(param, grad, buf, lr, momentum, dampening, weight_decay, nesterov, first,
+             grad_scale=1.0, shadow=None):
+    _lib.call("jmt_sgd_step", param.numel(), param.data_ptr(), grad.data_ptr(),
+              buf.data_ptr() if buf is not None else None, lr, momentum, dampening, weight_decay,
+              int(nesterov), int(first), grad_scale,
+              shadow.data_ptr() if shadow is not None else None,
+              dt(shadow) if shadow is not None else BF16, stream())

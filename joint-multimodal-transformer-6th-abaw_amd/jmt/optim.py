@@ -1,0 +1,77 @@
+"""Fused SGD over flat buffers (instantiator.py:32-38 semantics, config_file.json:73-80).
+
+All trainable parameters are re-homed into ONE flat fp32 buffer, their gradients into another
+(the buffer the RCCL all-reduce runs on), the momentum into a third; one jmt_sgd_step launch
+updates everything and rewrites the bf16/f16 compute shadows of the weights in the same pass.
+Parameters that never receive a gradient (the reference's unused `final_encoder`,
+`gated_attention`) must not be passed: torch.optim.SGD skips them because their .grad is None,
+so `used_parameters()` finds them with one probe backward."""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional
+
+import torch
+
+from . import functional as F
+from . import ops
+
+
+class FusedSGD:
+    def __init__(self, params: Iterable[torch.nn.Parameter], lr: float, momentum: float = 0.0,
+                 dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
+                 shadow_dtype: Optional[torch.dtype] = None):
+        self.params: List[torch.nn.Parameter] = list(params)
+        assert self.params, "no parameters"
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.numel = n
+        self.lr, self.momentum, self.dampening = lr, momentum, dampening
+        self.weight_decay, self.nesterov = weight_decay, nesterov
+        self.flat_p = torch.empty(n, dtype=torch.float32, device=dev)
+        self.flat_g = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.buf = torch.zeros(n, dtype=torch.float32, device=dev) if momentum else None
+        self.shadow = (torch.empty(n, dtype=shadow_dtype, device=dev)
+                       if shadow_dtype not in (None, torch.float32) else None)
+        off = 0
+        self._gviews = []
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                self.flat_p[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = self.flat_p[off:off + k].view_as(p)
+                g = self.flat_g[off:off + k].view_as(p)
+                p.grad = g
+                self._gviews.append(g)
+                off += k
+        if self.shadow is not None:
+            ops.cast(self.flat_p, self.shadow.dtype, out=self.shadow)
+            off = 0
+            for p in self.params:
+                k = p.numel()
+                F.register_shadow(p, self.shadow[off:off + k].view_as(p))
+                off += k
+        self.first = True
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat_g.zero_()
+        for p, g in zip(self.params, self._gviews):
+            if p.grad is None or p.grad.data_ptr() != g.data_ptr():
+                p.grad = g
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0):
+        ops.sgd_step(self.flat_p, self.flat_g, self.buf, self.lr, self.momentum, self.dampening,
+                     self.weight_decay, self.nesterov, self.first, grad_scale, self.shadow)
+        self.first = False
+
+
+def used_parameters(model_fn, params: Iterable[torch.nn.Parameter]):
+    """Run `model_fn()` (forward + backward), return the parameters that received a gradient."""
+    params = list(params)
+    for p in params:
+        p.grad = None
+    model_fn()
+    used = [p for p in params if p.grad is not None]
+    for p in params:
+        p.grad = None
+    return used

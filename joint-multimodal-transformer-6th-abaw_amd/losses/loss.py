@@ -1,0 +1,64 @@
+"""HIP-backed drop-in for the reference's losses/loss.py (CCCLoss is the training criterion,
+main.py:24,794).  No .cuda() in the constructors: the statistics run on the device of the
+predictions.  When jmt.dist has a loss group registered (one process per GPU), the CCC is the
+global-batch statistic, as under the reference's DataParallel gather."""
+import numpy as np
+import torch
+import torch.nn as nn
+
+from jmt import functional as F
+from jmt import dist as jdist
+
+
+class CCCLoss(nn.Module):
+    """loss.py:8-32: 1 - Lin's CCC of x (1,N) vs y (1,N); digitize_num>1: x is (N,k) logits,
+    expected value over bins = linspace(range) first."""
+
+    def __init__(self, digitize_num, range=[-1, 1], eps=1e-8):
+        super(CCCLoss, self).__init__()
+        self.digitize_num = digitize_num
+        self.range = range
+        self.eps = eps
+        if self.digitize_num != 0:
+            self.bins = torch.as_tensor(np.linspace(*self.range, num=self.digitize_num),
+                                        dtype=torch.float32).view((1, -1))
+
+    def forward(self, x, y):
+        return F.ccc_loss(x, y, eps=self.eps, digitize_num=self.digitize_num, rng=self.range,
+                          group=jdist.loss_group())
+
+
+class CELoss(nn.Module):
+    """loss.py:34-51: cross entropy against labels digitized into `digitize_num` bins.
+    (Off the training path of the shipped config; numpy digitize on the host as the reference.)"""
+
+    def __init__(self, digitize_num, range=[-1, 1], weights=None):
+        super(CELoss, self).__init__()
+        self.digitize_num = digitize_num
+        self.weights = torch.Tensor(weights) if weights is not None else None
+        assert self.digitize_num != 1
+        self.edges = np.linspace(*range, num=self.digitize_num + 1)
+
+    def forward(self, x, y):
+        y = y.view(-1)
+        y_dig = np.digitize(y.detach().cpu().numpy(), self.edges) - 1
+        y_dig[y_dig == self.digitize_num] = self.digitize_num - 1
+        yt = torch.as_tensor(y_dig, dtype=torch.long, device=x.device)
+        w = self.weights.to(x.device) if self.weights is not None else None
+        return torch.nn.functional.cross_entropy(x, yt, weight=w)
+
+
+class CCC_CE_Loss(nn.Module):
+    """loss.py:53-66."""
+
+    def __init__(self, digitize_num, range=[-1, 1], alpha=0.5, beta=0.5):
+        super(CCC_CE_Loss, self).__init__()
+        self.ccc_loss = CCCLoss(digitize_num, range=range)
+        self.ce_loss = CELoss(digitize_num, range=range)
+        self.alpha = alpha
+        self.beta = beta
+
+    def forward(self, x, y):
+        cccl = self.ccc_loss(x, y)
+        cel = self.ce_loss(x, y)
+        return self.alpha * cccl + self.beta * cel

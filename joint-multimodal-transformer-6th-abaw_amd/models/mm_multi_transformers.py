@@ -1,0 +1,147 @@
+"""HIP-backed drop-in for the reference's models/mm_multi_transformers.py.
+
+Same class names, constructor signatures, submodule names (hence state_dict keys) and forward
+semantics as the reference (file:line cited per class); every op runs on libjmt_hip.so kernels.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from jmt import functional as F
+from jmt.nn import Linear, LayerNorm, MLP, MultiheadAttention
+
+__all__ = ["Attention", "SequentialEncoder", "TransformerEncoderBlock",
+           "TransformerEncoderLayer", "MultimodalTransformer_w_JR", "FeatureConcatFC"]
+
+
+class Attention(nn.Module):
+    """Unused by the reference's models (mm_multi_transformers.py:7-26); kept for API parity."""
+
+    def __init__(self, input_dim):
+        super().__init__()
+        self.W = Linear(input_dim, input_dim)
+        self.V = Linear(input_dim, input_dim, bias=False)
+        self.tanh = nn.Tanh()
+        self.fc = Linear(input_dim, 2)
+        self.out_layer1 = Linear(512, 256)
+        self.out_layer2 = Linear(256, 64)
+        self.out_layer3 = Linear(64, 2)
+
+    def forward(self, x):
+        raise NotImplementedError("dead code in the reference (never called)")
+
+
+class SequentialEncoder(nn.Sequential):
+    """mm_multi_transformers.py:29-33."""
+
+    def forward(self, x):
+        for module in self._modules.values():
+            x = module(x)
+        return x
+
+
+class TransformerEncoderLayer(nn.Module):
+    """Post-LN encoder layer, mm_multi_transformers.py:48-70:
+    x = LN1(x + MHA(x, x, x)); x = LN2(x + W2 relu(W1 x + b1) + b2)."""
+
+    def __init__(self, input_dim, num_heads, hidden_dim):
+        super().__init__()
+        self.attention = MultiheadAttention(input_dim, num_heads)
+        self.feed_forward = MLP(input_dim, hidden_dim, input_dim)
+        self.layer_norm1 = LayerNorm(input_dim)
+        self.layer_norm2 = LayerNorm(input_dim)
+
+    def forward(self, x):
+        attn_output, _ = self.attention(x, x, x)
+        x = self.layer_norm1(x, attn_output)
+        ff_output = self.feed_forward(x)
+        return self.layer_norm2(x, ff_output)
+
+
+class TransformerEncoderBlock(nn.Module):
+    """mm_multi_transformers.py:36-45."""
+
+    def __init__(self, input_dim, num_heads, hidden_dim, num_layers):
+        super().__init__()
+        self.layers = SequentialEncoder(
+            *[TransformerEncoderLayer(input_dim, num_heads, hidden_dim) for _ in range(num_layers)])
+
+    def forward(self, x):
+        return self.layers(x)
+
+
+class MultimodalTransformer_w_JR(nn.Module):
+    """JMT with joint representation, mm_multi_transformers.py:73-214.
+
+    forward(visual (B,T,512), physiological (B,T,512)):
+      FC head         -> (T, B, 1024) seq-first (the reference's layout quirk, kept)
+      SELF_ATTEN head -> (B, T, 512)
+    `final_encoder` (E=3072) is constructed and never called, as in the reference (:92-93)."""
+
+    def __init__(self, visual_dim, audio_dim, num_heads, hidden_dim, num_layers,
+                 output_format: str):
+        super().__init__()
+        assert output_format in ["FC", "SELF_ATTEN"], output_format
+        self.output_format = output_format
+        self.num_heads = num_heads
+        self.visual_encoder = TransformerEncoderBlock(visual_dim, num_heads, hidden_dim,
+                                                      num_layers)
+        self.physiological_encoder = TransformerEncoderBlock(audio_dim, num_heads, hidden_dim,
+                                                             num_layers)
+        self.joint_representation_encoder = TransformerEncoderBlock(audio_dim, num_heads,
+                                                                    hidden_dim, num_layers)
+        self.final_encoder = TransformerEncoderBlock(3072, num_heads, hidden_dim, num_layers)
+        self.cross_attention_v = MultiheadAttention(visual_dim, num_heads)
+        self.cross_attention_p = MultiheadAttention(audio_dim, num_heads)
+        self.cross_attention_pv = MultiheadAttention(512, num_heads)
+        self.out_layer_pv = Linear(1024, 512)
+        if output_format == "FC":
+            self.out_layer1 = Linear(3072, 1024)
+        elif output_format == "SELF_ATTEN":
+            self.final_visual_encoder = TransformerEncoderBlock(visual_dim, num_heads, hidden_dim,
+                                                                num_layers)
+            self.final_self_attention = MultiheadAttention(512, num_heads)
+        else:
+            raise NotImplementedError(output_format)
+
+    def forward(self, visual_features, physiological_features):
+        # cat + out_layer_pv as ONE K-concatenated GEMM (:120-124)
+        joint_representation = F.linear((visual_features, physiological_features),
+                                        self.out_layer_pv.weight, self.out_layer_pv.bias)
+        v = visual_features.permute(1, 0, 2)          # free: a strided view (:127-129)
+        p = physiological_features.permute(1, 0, 2)
+        j = joint_representation.permute(1, 0, 2)
+        v = self.visual_encoder(v)
+        p = self.physiological_encoder(p)
+        j = self.joint_representation_encoder(j)
+        ca_v, ca_p, ca_pv = self.cross_attention_v, self.cross_attention_p, self.cross_attention_pv
+        outs = [ca_v(v, p, p)[0],      # :142-167 (key is value in every call)
+                ca_p(p, v, v)[0],
+                ca_pv(j, v, v)[0],
+                ca_v(v, j, j)[0],
+                ca_pv(j, p, p)[0],
+                ca_p(p, j, j)[0]]
+        if self.output_format == "SELF_ATTEN":
+            # :169-199 — stack to (6, B*T, 512), encoder over the 6-token sequences, MHA, keep
+            # token 5.  Only the last query row of the final attention is computed: it is the
+            # only one the reference keeps ([:, :, -1, :], :193).
+            T, B, E = outs[0].shape
+            st = F.stack_seq(outs, seq_first_in=True)
+            enc = self.final_visual_encoder(st)
+            last = enc[-1:]
+            fa, _ = self.final_self_attention(last, enc, enc)
+            return fa[0].reshape(B, T, E)
+        # FC head (:201-211): torch.cat of the 6 outputs never materialised (K-concat GEMM)
+        return F.linear(tuple(outs), self.out_layer1.weight, self.out_layer1.bias)
+
+
+class FeatureConcatFC(nn.Module):
+    """mm_multi_transformers.py:217-224: fc(cat(v, a))."""
+
+    def __init__(self, visual_dim, audio_dim):
+        super().__init__()
+        self.fc = Linear(visual_dim + audio_dim, 512)
+
+    def forward(self, visual_features, audio_features):
+        return F.linear((visual_features, audio_features), self.fc.weight, self.fc.bias)

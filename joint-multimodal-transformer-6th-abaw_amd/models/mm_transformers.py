@@ -1,0 +1,46 @@
+"""HIP-backed drop-in for the reference's models/mm_transformers.py (no comet_ml / torchvision /
+matplotlib imports: they are unused there, mm_transformers.py:2-18)."""
+from __future__ import annotations
+
+import torch.nn as nn
+
+from jmt import functional as F
+from jmt.nn import Linear
+
+from .mm_multi_transformers import (Attention, SequentialEncoder, TransformerEncoderBlock,
+                                    TransformerEncoderLayer)
+from .mm_multi_transformers import MultiheadAttention
+
+__all__ = ["Attention", "SequentialEncoder", "TransformerEncoderBlock",
+           "TransformerEncoderLayer", "MultimodalTransformer_wo_JR"]
+
+
+class MultimodalTransformer_wo_JR(nn.Module):
+    """JMT without joint representation, mm_transformers.py:87-146.
+
+    The encoders receive (B, T, D) directly, i.e. self-attention runs over the BATCH axis
+    (seq = B, batch = T) exactly as in the reference (:120-122); the cross-attentions permute to
+    (T, B, D) (:125-135).  `gated_attention` is constructed and unused (:103)."""
+
+    def __init__(self, visual_dim, audio_dim, num_heads, hidden_dim, num_layers,
+                 output_format: str):
+        super().__init__()
+        assert output_format in ['FC'], output_format
+        self.output_format = output_format
+        self.visual_encoder = TransformerEncoderBlock(visual_dim, num_heads, hidden_dim,
+                                                      num_layers)
+        self.physiological_encoder = TransformerEncoderBlock(audio_dim, num_heads, hidden_dim,
+                                                             num_layers)
+        self.cross_attention_v = MultiheadAttention(visual_dim, num_heads)
+        self.cross_attention_p = MultiheadAttention(audio_dim, num_heads)
+        self.gated_attention = Linear(visual_dim + audio_dim, 1)
+        self.final_layer = Linear(1024, 512)
+
+    def forward(self, visual_features, physiological_features):
+        v = self.visual_encoder(visual_features)
+        p = self.physiological_encoder(physiological_features)
+        vt, pt = v.permute(1, 0, 2), p.permute(1, 0, 2)
+        ov = self.cross_attention_v(vt, pt, pt)[0].permute(1, 0, 2)
+        op = self.cross_attention_p(pt, vt, vt)[0].permute(1, 0, 2)
+        assert self.output_format == 'FC', self.output_format
+        return F.linear((ov, op), self.final_layer.weight, self.final_layer.bias)

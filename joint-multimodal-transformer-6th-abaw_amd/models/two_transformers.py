@@ -1,0 +1,103 @@
+"""HIP-backed drop-in for the reference's models/two_transformers.py."""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+from torch import nn
+
+from jmt import functional as F
+from jmt.nn import Linear, MLP
+
+from .mm_multi_transformers import MultimodalTransformer_w_JR
+from .mm_multi_transformers import FeatureConcatFC
+from .mm_transformers import MultimodalTransformer_wo_JR
+
+__all__ = ['Two_transformers', 'SingleBackbonePretrainer']
+
+
+class Two_transformers(nn.Module):
+    """two_transformers.py:17-128.  forward(f1_norm=audio, f2_norm=video) -> (vouts, aouts),
+    (T, B) for TRANSFORMER/FC and (B, T) otherwise — the reference's layouts, reproduced."""
+
+    def __init__(self, v_dropout: float, a_dropout: float, num_heads: int, num_layers: int,
+                 joint_modalities: str, output_format: str = 'FC', vision_in_ft: int = 512):
+        super(Two_transformers, self).__init__()
+        assert isinstance(v_dropout, float), type(v_dropout)
+        assert 0.0 <= v_dropout < 1., v_dropout
+        self.v_dropout = v_dropout
+        assert isinstance(a_dropout, float), type(a_dropout)
+        assert 0.0 <= a_dropout < 1., a_dropout
+        self.a_dropout = a_dropout
+        assert isinstance(num_heads, int), type(num_heads)
+        assert num_heads > 0, num_heads
+        self.num_heads = num_heads
+        assert isinstance(num_layers, int), type(num_layers)
+        assert num_layers > 0, num_layers
+        self.num_layers = num_layers
+        assert isinstance(joint_modalities, str), type(joint_modalities)
+        assert joint_modalities in ['NONE', 'TRANSFORMER', 'FC'], joint_modalities
+        self.joint_modalities = joint_modalities
+        assert isinstance(vision_in_ft, int), type(vision_in_ft)
+        assert vision_in_ft > 0, vision_in_ft
+        self.vision_in_ft = vision_in_ft
+
+        self.linear = None
+        if vision_in_ft != 512:
+            self.linear = Linear(vision_in_ft, 512)
+
+        assert output_format in ['FC', 'SELF_ATTEN'], output_format
+        self.output_format = output_format
+
+        if joint_modalities == 'TRANSFORMER':
+            self.mm_transformer = MultimodalTransformer_w_JR(
+                visual_dim=512, audio_dim=512, num_heads=num_heads, hidden_dim=512,
+                num_layers=num_layers, output_format=output_format)
+            dim = 1024 if output_format == 'FC' else 512
+        elif joint_modalities == 'FC':
+            self.mm_transformer = FeatureConcatFC(512, 512)
+            dim = 512
+        elif joint_modalities == 'NONE':
+            assert output_format in ['FC'], output_format
+            self.mm_transformer = MultimodalTransformer_wo_JR(
+                visual_dim=512, audio_dim=512, num_heads=num_heads, hidden_dim=512,
+                num_layers=num_layers, output_format=output_format)
+            dim = 512
+        else:
+            raise NotImplementedError(joint_modalities)
+
+        self.vregressor = MLP(dim, 128, 1, dropout=v_dropout)
+        self.aregressor = MLP(dim, 128, 1, dropout=a_dropout)
+
+    def forward(self, f1_norm, f2_norm):
+        video = F.l2_normalize(f2_norm)          # :118
+        audio = F.l2_normalize(f1_norm)          # :119
+        if self.linear is not None:
+            video = self.linear(video)           # :120-121
+        av = self.mm_transformer(video, audio)
+        # regressors in fp32 out (predictions feed the fp32 CCC statistics)
+        vouts = self.vregressor(av, out_dtype=torch.float32).squeeze(2)
+        aouts = self.aregressor(av, out_dtype=torch.float32).squeeze(2)
+        if not vouts.is_contiguous():             # seq-first (T,B) views -> contiguous (T,B)
+            vouts = F.TransposeCopyFn.apply(vouts)
+            aouts = F.TransposeCopyFn.apply(aouts)
+        return vouts, aouts
+
+
+class SingleBackbonePretrainer(nn.Module):
+    """two_transformers.py:131-162 (PRETRAINING goal only)."""
+
+    def __init__(self, v_dropout: float, a_dropout: float):
+        super(SingleBackbonePretrainer, self).__init__()
+        assert isinstance(v_dropout, float), type(v_dropout)
+        assert 0.0 <= v_dropout < 1., v_dropout
+        self.v_dropout = v_dropout
+        assert isinstance(a_dropout, float), type(a_dropout)
+        assert 0.0 <= a_dropout < 1., a_dropout
+        self.a_dropout = a_dropout
+        self.regressor = MLP(512, 128, 2, dropout=a_dropout)
+
+    def forward(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        assert x.ndim == 3, x.ndim
+        out = self.regressor(x, out_dtype=torch.float32)
+        return out[:, :, 0], out[:, :, 1]

@@ -1,0 +1,302 @@
+"""Kernel-level numerics on the MI355X: every HIP kernel vs a plain PyTorch fp32 reference of the
+same op (computed from the same, already-rounded inputs), through the C-ABI."""
+import math
+
+import pytest
+import torch
+
+from jmt import functional as JF
+from jmt import ops
+from jmt._lib import BF16, F16, F32
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TD = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16}
+
+
+def _rup(a, b):
+    return -(-a // b) * b
+
+
+def _tol(dt, K):
+    # fp32: exact-f32 MFMA chain; 16-bit: inputs exact, fp32 accumulate -> only order effects
+    return 2e-5 * math.sqrt(max(K, 1)) if dt == F32 else 2e-4 * math.sqrt(max(K, 1))
+
+
+def _operand(rows, cols, kmajor_rows, dt, batch=1, gen=None):
+    """Logical X[b] (rows x cols) stored row-major with padded ld if kmajor_rows, else stored
+    transposed (cols x rows) with padded ld.  Returns (storage, logical_fp32, ld, batch_stride)."""
+    t = TD[dt]
+    if kmajor_rows:
+        ld = _rup(cols, 8) + 8
+        st = torch.randn(batch, rows, ld, device=DEV, generator=gen).to(t)
+        logical = st[:, :, :cols].float()
+    else:
+        ld = _rup(rows, 8) + 8
+        st = torch.randn(batch, cols, ld, device=DEV, generator=gen).to(t)
+        logical = st[:, :, :rows].float().transpose(1, 2)
+    return st, logical, ld, st.stride(0)
+
+
+SHAPES = [(128, 128, 64), (300, 300, 512), (37, 53, 300), (19, 1, 128), (1, 128, 37),
+          (200, 72, 130), (256, 512, 1024)]
+
+
+@pytest.mark.parametrize("dt", [F32, BF16, F16])
+@pytest.mark.parametrize("ak", [True, False])
+@pytest.mark.parametrize("bk", [True, False])
+def test_gemm_layouts_dtypes(dt, ak, bk):
+    g = torch.Generator(device=DEV).manual_seed(1)
+    for (M, N, K) in SHAPES:
+        A, Al, lda, sa = _operand(M, K, ak, dt, gen=g)
+        # B logical K x N; "b_kmajor" = stored [N][K]
+        Bs, Bl_t, ldb, sb = _operand(N, K, bk, dt, gen=g)
+        Bl = Bl_t.transpose(1, 2)
+        C = torch.full((M, N + 3), float("nan"), device=DEV)
+        ops.gemm(M=M, N=N, K=K, ab_dtype=dt, c_dtype=F32, a=[A.data_ptr()], lda=lda, a_kmajor=ak,
+                 b=[Bs.data_ptr()], ldb=ldb, b_kmajor=bk, c=[C.data_ptr()], ldc=N + 3,
+                 splits=1, device=DEV)
+        ref = Al[0] @ Bl[0]
+        err = (C[:, :N] - ref).abs().max().item()
+        assert err <= _tol(dt, K) * max(1.0, ref.abs().max().item()), (M, N, K, err)
+        assert torch.isnan(C[:, N:]).all(), "wrote outside N"
+
+
+@pytest.mark.parametrize("dt", [F32, BF16])
+def test_gemm_epilogues_and_splitk(dt):
+    g = torch.Generator(device=DEV).manual_seed(2)
+    M, N, K = 333, 200, 1000
+    A, Al, lda, _ = _operand(M, K, True, dt, gen=g)
+    Bs, Bl_t, ldb, _ = _operand(N, K, True, dt, gen=g)
+    Bl = Bl_t.transpose(1, 2)[0]
+    base = Al[0] @ Bl
+    bias = torch.randn(N, device=DEV, generator=g)
+    biasr = torch.randn(M, device=DEV, generator=g)
+    for splits in (1, 4):
+        # bias per column + relu, out in the ab dtype
+        C = torch.empty(M, N, device=DEV, dtype=TD[dt])
+        ops.gemm(M=M, N=N, K=K, ab_dtype=dt, c_dtype=dt, a=[A.data_ptr()], lda=lda, a_kmajor=True,
+                 b=[Bs.data_ptr()], ldb=ldb, b_kmajor=True, c=[C.data_ptr()], ldc=N,
+                 bias=bias, bias_mode=1, relu=True, splits=splits, device=DEV)
+        ref = torch.relu(base + bias)
+        tol = _tol(dt, K) * ref.abs().max().item() + (0 if dt == F32 else 8e-3 * ref.abs().max().item())
+        assert (C.float() - ref).abs().max().item() <= tol
+        # alpha, row bias, beta accumulate into fp32
+        C0 = torch.randn(M, N, device=DEV, generator=g)
+        C = C0.clone()
+        ops.gemm(M=M, N=N, K=K, ab_dtype=dt, c_dtype=F32, a=[A.data_ptr()], lda=lda, a_kmajor=True,
+                 b=[Bs.data_ptr()], ldb=ldb, b_kmajor=True, c=[C.data_ptr()], ldc=N,
+                 alpha=0.5, beta=1.0, bias=biasr, bias_mode=2, splits=splits, device=DEV)
+        ref = 0.5 * base + biasr[:, None] + C0
+        assert (C - ref).abs().max().item() <= _tol(dt, K) * ref.abs().max().item()
+        # aux mask (ReLU backward): zero where aux <= 0
+        aux = torch.randn(M, N, device=DEV, generator=g).to(TD[dt])
+        C = torch.empty(M, N, device=DEV)
+        ops.gemm(M=M, N=N, K=K, ab_dtype=dt, c_dtype=F32, a=[A.data_ptr()], lda=lda, a_kmajor=True,
+                 b=[Bs.data_ptr()], ldb=ldb, b_kmajor=True, c=[C.data_ptr()], ldc=N, aux=aux,
+                 ldaux=N, splits=splits, device=DEV)
+        ref = torch.where(aux.float() > 0, base, torch.zeros_like(base))
+        assert (C - ref).abs().max().item() <= _tol(dt, K) * base.abs().max().item()
+
+
+@pytest.mark.parametrize("dt", [F32, BF16])
+def test_gemm_batched_two_level_strides(dt):
+    """attention-shaped: S[n,h] = Q[n,h] K[n,h]^T on seq-first (L, N, H*dh) packed buffers."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    L, Nb, H, dh = 45, 3, 4, 64
+    t = TD[dt]
+    qkv = torch.randn(Nb, L, 3 * H * dh, device=DEV, generator=g).to(t)   # (N, L, 3E) memory
+    E = H * dh
+    S = torch.empty(Nb, H, L, 48, device=DEV)
+    ops.gemm(M=L, N=L, K=dh, ab_dtype=dt, c_dtype=F32,
+             a=[qkv.data_ptr()], lda=3 * E, a_kmajor=True, sA=(L * 3 * E, dh),
+             b=[qkv.data_ptr() + E * qkv.element_size()], ldb=3 * E, b_kmajor=True,
+             sB=(L * 3 * E, dh), c=[S.data_ptr()], ldc=48, sC=(H * L * 48, L * 48),
+             batch0=Nb, batch1=H, device=DEV)
+    q = qkv[..., :E].float().view(Nb, L, H, dh).permute(0, 2, 1, 3)
+    k = qkv[..., E:2 * E].float().view(Nb, L, H, dh).permute(0, 2, 1, 3)
+    ref = q @ k.transpose(-1, -2)
+    assert (S[..., :L] - ref).abs().max().item() <= _tol(dt, dh) * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("dt", [F32, BF16])
+def test_gemm_kconcat_and_pointer_tables(dt):
+    g = torch.Generator(device=DEV).manual_seed(4)
+    t = TD[dt]
+    M, seg, nseg, N = 150, 64 if dt == BF16 else 32, 6, 96
+    xs = [torch.randn(M, seg, device=DEV, generator=g).to(t) for _ in range(nseg)]
+    W = torch.randn(N, seg * nseg, device=DEV, generator=g).to(t)
+    C = torch.empty(M, N, device=DEV)
+    ops.gemm(M=M, N=N, K=seg * nseg, ab_dtype=dt, c_dtype=F32, a=[x.data_ptr() for x in xs],
+             lda=seg, a_kmajor=True, a_mode=2, a_kseg=seg, b=[W.data_ptr()], ldb=seg * nseg,
+             b_kmajor=True, c=[C.data_ptr()], ldc=N, device=DEV)
+    ref = torch.cat([x.float() for x in xs], 1) @ W.float().t()
+    assert (C - ref).abs().max().item() <= _tol(dt, seg * nseg) * ref.abs().max().item()
+    # dgrad-style: outs[s] = dY @ W[:, s] with a C pointer table and B batch stride
+    dY = torch.randn(M, N, device=DEV, generator=g).to(t)
+    outs = [torch.empty(M, seg, device=DEV) for _ in range(nseg)]
+    ops.gemm(M=M, N=seg, K=N, ab_dtype=dt, c_dtype=F32, a=[dY.data_ptr()], lda=N, a_kmajor=True,
+             b=[W.data_ptr()], ldb=seg * nseg, b_kmajor=False, c=[o.data_ptr() for o in outs],
+             ldc=seg, c_mode=1, batch0=nseg, sB=(seg, 0), device=DEV)
+    full = dY.float() @ W.float()
+    for s in range(nseg):
+        r = full[:, s * seg:(s + 1) * seg]
+        assert (outs[s] - r).abs().max().item() <= _tol(dt, N) * full.abs().max().item()
+    # wgrad-style: dW[:, s] += dY^T X_s with a B pointer table, split-K over M
+    dW = torch.randn(N, seg * nseg, device=DEV, generator=g)
+    dW0 = dW.clone()
+    ops.gemm(M=N, N=seg, K=M, ab_dtype=dt, c_dtype=F32, a=[dY.data_ptr()], lda=N, a_kmajor=False,
+             b=[x.data_ptr() for x in xs], ldb=seg, b_kmajor=False, b_mode=1,
+             c=[dW.data_ptr()], ldc=seg * nseg, batch0=nseg, sC=(seg, 0), beta=1.0, splits=3,
+             device=DEV)
+    ref = dW0 + dY.float().t() @ torch.cat([x.float() for x in xs], 1)
+    assert (dW - ref).abs().max().item() <= _tol(dt, M) * ref.abs().max().item()
+
+
+def test_gemm_large_bf16_linear_shape():
+    """The benchmark's dominant shape: (19200 x 1024) @ (1024 x 512)^T in bf16."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    X = torch.randn(19200, 1024, device=DEV, generator=g).bfloat16()
+    W = torch.randn(512, 1024, device=DEV, generator=g).bfloat16()
+    Y = torch.empty(19200, 512, device=DEV, dtype=torch.bfloat16)
+    ops.gemm(M=19200, N=512, K=1024, ab_dtype=BF16, c_dtype=BF16, a=[X.data_ptr()], lda=1024,
+             a_kmajor=True, b=[W.data_ptr()], ldb=1024, b_kmajor=True, c=[Y.data_ptr()], ldc=512,
+             device=DEV)
+    ref = X.float() @ W.float().t()
+    rel = ((Y.float() - ref).abs().max() / ref.abs().max()).item()
+    assert rel < 1e-2
+
+
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_l2norm_fwd_bwd(cd):
+    g = torch.Generator(device=DEV).manual_seed(6)
+    x = torch.randn(5, 37, 2048, device=DEV, generator=g)
+    x[0, 0] = 0.0                                      # the eps-clamped branch
+    x.requires_grad_(True)
+    with JF.compute_mode(cd):
+        y = JF.l2_normalize(x)
+        gy = torch.randn(y.shape, device=DEV, generator=g).to(cd)
+        y.backward(gy)
+    xr = x.detach().clone().requires_grad_(True)
+    yr = torch.nn.functional.normalize(xr, dim=-1)
+    yr.backward(gy.float())
+    tol = 1e-6 if cd == torch.float32 else 1e-2
+    assert (y.float() - yr).abs().max().item() <= tol * yr.abs().max().item() + 1e-7
+    assert (x.grad - xr.grad).abs().max().item() <= tol * xr.grad.abs().max().item() + 1e-7
+
+
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("D", [512, 768])
+def test_add_layernorm_fwd_bwd(cd, D):
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = (torch.randn(300, 7, D, device=DEV, generator=g) * 3 + 1).to(cd).requires_grad_(True)
+    r = torch.randn(300, 7, D, device=DEV, generator=g).to(cd).requires_grad_(True)
+    gam = torch.nn.Parameter(1 + 0.1 * torch.randn(D, device=DEV, generator=g))
+    bet = torch.nn.Parameter(0.1 * torch.randn(D, device=DEV, generator=g))
+    with JF.compute_mode(cd):
+        y = JF.add_layer_norm(x, r, gam, bet, 1e-5)
+    gy = torch.randn(y.shape, device=DEV, generator=g).to(cd)
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True)
+    g2 = gam.detach().clone().requires_grad_(True)
+    b2 = bet.detach().clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr + rr, (D,), g2, b2, 1e-5)
+    yr.backward(gy.float())
+    tol = 2e-5 if cd == torch.float32 else 2e-2
+    assert (y.float() - yr).abs().max().item() <= tol * yr.abs().max().item()
+    assert (x.grad.float() - xr.grad).abs().max().item() <= tol * xr.grad.abs().max().item()
+    assert (r.grad.float() - rr.grad).abs().max().item() <= tol * rr.grad.abs().max().item()
+    assert (gam.grad - g2.grad).abs().max().item() <= tol * g2.grad.abs().max().item()
+    assert (bet.grad - b2.grad).abs().max().item() <= tol * b2.grad.abs().max().item()
+
+
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H,Lq,Lk,N", [(1, 300, 300, 3), (8, 37, 37, 2), (1, 1, 6, 40),
+                                       (4, 64, 17, 5)])
+def test_attention_core_fwd_bwd(cd, H, Lq, Lk, N):
+    """q/k/v as slices of packed projections in a (N, L, *) memory layout (seq-first views)."""
+    g = torch.Generator(device=DEV).manual_seed(8)
+    E = 512 if H in (1, 4) else 256
+    qsrc = torch.randn(N, Lq, E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    kv = torch.randn(N, Lk, 2 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    qsrc.requires_grad_(True)
+    kv.requires_grad_(True)
+    with JF.compute_mode(cd):
+        o = JF.AttnCoreFn.apply(qsrc, kv, kv, E, H, 0, 0, E)
+    go = torch.randn(o.shape, device=DEV, generator=g).to(cd)
+    o.backward(go)
+    dh = E // H
+    qr = qsrc.detach().float().requires_grad_(True)
+    kvr = kv.detach().float().requires_grad_(True)
+    q = qr.reshape(Lq, N * H, dh).transpose(0, 1) / math.sqrt(dh)
+    k = kvr[..., :E].reshape(Lk, N * H, dh).transpose(0, 1)
+    v = kvr[..., E:].reshape(Lk, N * H, dh).transpose(0, 1)
+    ref = (torch.softmax(q @ k.transpose(1, 2), -1) @ v).transpose(0, 1).reshape(Lq, N, E)
+    ref.backward(go.float())
+    tol = 5e-5 if cd == torch.float32 else 3e-2
+    assert (o.float() - ref).abs().max().item() <= tol * ref.abs().max().item()
+    assert (qsrc.grad.float() - qr.grad).abs().max().item() <= tol * qr.grad.abs().max().item()
+    assert (kv.grad.float() - kvr.grad).abs().max().item() <= tol * kvr.grad.abs().max().item()
+
+
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_linear_mlp_autograd(cd):
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = torch.randn(40, 3, 1024, device=DEV, generator=g).permute(1, 0, 2).requires_grad_(True)
+    W1 = torch.nn.Parameter(torch.randn(128, 1024, device=DEV, generator=g) * 0.03)
+    b1 = torch.nn.Parameter(torch.randn(128, device=DEV, generator=g) * 0.1)
+    W2 = torch.nn.Parameter(torch.randn(1, 128, device=DEV, generator=g) * 0.1)
+    b2 = torch.nn.Parameter(torch.randn(1, device=DEV, generator=g) * 0.1)
+    with JF.compute_mode(cd):
+        y = JF.mlp(x, W1, b1, W2, b2, out_dtype=torch.float32)
+    gy = torch.randn(y.shape, device=DEV, generator=g)
+    y.backward(gy)
+    ps = [t.detach().clone().requires_grad_(True) for t in (x, W1, b1, W2, b2)]
+    yr = torch.relu(ps[0] @ ps[1].t() + ps[2]) @ ps[3].t() + ps[4]
+    yr.backward(gy)
+    tol = 3e-5 if cd == torch.float32 else 3e-2
+    assert y.shape == yr.shape
+    assert (y - yr).abs().max().item() <= tol * yr.abs().max().item()
+    for a, b in zip((x, W1, b1, W2, b2), ps):
+        assert (a.grad.float() - b.grad).abs().max().item() <= tol * b.grad.abs().max().item()
+
+
+def test_softmax_rows_and_padding():
+    g = torch.Generator(device=DEV).manual_seed(10)
+    S = torch.randn(50, 304, device=DEV, generator=g) * 4
+    P = torch.full((50, 304), 7.0, device=DEV, dtype=torch.bfloat16)
+    ops.softmax_fwd(S, 304, 50, 300, 0.5, P, 304)
+    ref = torch.softmax(S[:, :300] * 0.5, -1)
+    assert (P[:, :300].float() - ref).abs().max().item() < 4e-3
+    assert (P[:, 300:] == 0).all()
+
+
+def test_colsum_and_copy2d():
+    g = torch.Generator(device=DEV).manual_seed(11)
+    dy = torch.randn(19201, 96, device=DEV, generator=g).bfloat16()
+    db = torch.ones(96, device=DEV)
+    ops.colsum(dy, 96, 19201, 96, db, beta_acc=True)
+    ref = 1 + dy.float().sum(0)
+    assert (db - ref).abs().max().item() < 1e-3
+    x = torch.randn(37, 5, device=DEV, generator=g)
+    y = torch.empty(5, 37, device=DEV, dtype=torch.bfloat16)
+    ops.copy2d(x.data_ptr(), F32, y.data_ptr(), BF16, 37, 5, 5, 1, 1, 37)
+    assert (y.float() - x.t().bfloat16().float()).abs().max().item() == 0
+
+
+def test_sgd_matches_torch_nesterov():
+    g = torch.Generator(device=DEV).manual_seed(12)
+    p = torch.randn(10007, device=DEV, generator=g)
+    p_ref = p.clone().requires_grad_(True)
+    opt = torch.optim.SGD([p_ref], lr=1e-2, momentum=0.9, dampening=0.0, weight_decay=1e-4,
+                          nesterov=True)
+    buf = torch.zeros_like(p)
+    shadow = torch.empty(10007, device=DEV, dtype=torch.bfloat16)
+    for step in range(3):
+        gr = torch.randn(10007, device=DEV, generator=g)
+        ops.sgd_step(p, gr * 2.0, buf, 1e-2, 0.9, 0.0, 1e-4, True, step == 0, 0.5, shadow)
+        p_ref.grad = gr.clone()
+        opt.step()
+    assert (p - p_ref.detach()).abs().max().item() < 1e-6
+    assert (shadow.float() - p.bfloat16().float()).abs().max().item() == 0
