@@ -1,0 +1,249 @@
+"""Training-step throughput of the JMT fusion hot path on MI355X (BASELINE.json metric:
+"train windows/sec + CCC parity, B=64 T=300 A/V fusion, 1/2/4/8 MI355X").
+
+Workload (BASELINE.json configs[2], the one the metric is quoted on): per GPU B=64 windows of
+T=300 synthetic backbone features (audio D_a=1024, video D_v=2048, N(0,1), resident in HBM),
+FcLayer(1024,512) on the audio (main.py:379) -> Two_transformers(0,0,H=1,L=1,'TRANSFORMER','FC',
+vision_in_ft=2048) -> 2x losses.loss.CCCLoss(1) (global-batch statistics) -> backward -> RCCL
+all-reduce of the flat gradient (N>1) -> fused SGD-nesterov step (config_file.json:73-80).
+Random-init weights.  bf16 MFMA compute, fp32 master weights / statistics.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+
+Prints ONE JSON line (rank 0).  `value` = windows/s of the whole job (weak scaling: B=64 per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "joint-multimodal-transformer-6th-abaw_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2516.6      # 256 CU x 4 SIMD x 1024 flop/clk (16x16x32 bf16 / 16 cyc) x 2.4 GHz
+PEAK_HBM_GBS = 8000.0
+D_A, D_V, E = 1024, 2048, 512
+
+
+def step_flops(B: int, T: int) -> float:
+    """Algorithmic matmul FLOPs of one training step (SURVEY.md §8d closed form, TRANSFORMER/FC,
+    L=1, h=d, plus the FcLayer): W = 3F - 2*T*d*(D_a+D_v) per window."""
+    d = E
+    F = (2 * T * d * (D_A + D_V) + 4 * T * d * d + 3 * (12 * T * d * d + 4 * T * T * d)
+         + 6 * (8 * T * d * d + 4 * T * T * d) + 24 * T * d * d + 4 * T * 1024 * 128 + 4 * T * 128)
+    W = 3 * F - 2 * T * d * (D_A + D_V)
+    return W * B
+
+
+class GemmProbe:
+    """HIP-event timing of every launch of the dominant GEMM instance inside the timed region
+    (events recorded on the stream the kernels are launched on: torch's current stream)."""
+
+    def __init__(self, key):
+        self.key = key
+        self.on = False
+        self.events = []
+        self.flops = []
+
+    def __call__(self, info, launch):
+        if not self.on or (info["ab_dtype"], info["a_kmajor"], info["b_kmajor"]) != self.key:
+            return launch()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = launch()
+        e.record()
+        self.events.append((s, e))
+        self.flops.append(2.0 * info["M"] * info["N"] * info["K"] * info["batch"])
+        return r
+
+    def summary(self):
+        if not self.events:
+            return None
+        ms = [s.elapsed_time(e) for s, e in self.events]
+        return {"launches": len(ms), "avg_ms": sum(ms) / len(ms),
+                "avg_flops": sum(self.flops) / len(self.flops),
+                "total_ms": sum(ms)}
+
+
+def cpu_baseline(model_sd, fc_sd, B, T, steps=2):
+    """The oracle (CPU restatement, oracle/jmt_ref.py) timed on this host: fp32 torch-CPU
+    forward+backward+SGD of the same step on a bounded sample (B windows, 1 warm-up)."""
+    from oracle import jmt_ref as R
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(16, ncpu))
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(1234)
+    audio = torch.randn(B, T, D_A, generator=g)
+    video = torch.randn(B, T, D_V, generator=g)
+    lv = torch.rand(B, T, generator=g) * 2 - 1
+    la = torch.rand(B, T, generator=g) * 2 - 1
+    p = {k: v.detach().float().cpu().clone() for k, v in model_sd.items()}
+    fp = {k: v.detach().float().cpu().clone() for k, v in fc_sd.items()}
+    bufs = {}
+    times = []
+    for i in range(steps + 1):
+        t0 = time.perf_counter()
+        R.train_step(p, fp, audio, video, lv, la, 1, 1, "TRANSFORMER", "FC", 2048, bufs)
+        times.append(time.perf_counter() - t0)
+    t = sum(times[1:]) / steps
+    return {"value": round(B / t, 3), "unit": "windows/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/jmt_ref.py train_step, B={B} T={T} fp32 torch-CPU, 1 warm-up + "
+                      f"{steps} timed steps ({t * 1e3:.0f} ms/step)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="windows per GPU")
+    ap.add_argument("--seq", type=int, default=300)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=64)
+    ap.add_argument("--no-probe", action="store_true", help="no per-launch events (profiling)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from jmt import functional as JF
+    from jmt import ops
+    from jmt import dist as jdist
+    from jmt.optim import FusedSGD, used_parameters
+    from models.two_transformers import Two_transformers
+    from models.fc_layer import FcLayer
+    from losses.loss import CCCLoss
+
+    cd = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
+    B, T = args.batch, args.seq
+    torch.manual_seed(0)
+    model = Two_transformers(0.0, 0.0, 1, 1, "TRANSFORMER", "FC", D_V).to(dev)
+    fc = FcLayer(D_A, E).to(dev)
+    model_sd0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()} \
+        if rank == 0 else None
+    fc_sd0 = {k: v.detach().cpu().clone() for k, v in fc.state_dict().items()} \
+        if rank == 0 else None
+    if world > 1:
+        jdist.set_loss_group(dist.group.WORLD)
+
+    # synthetic inputs resident in HBM, disjoint per rank (global batch = world * B)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    audio = torch.randn(B, T, D_A, device=dev, generator=g)
+    video = torch.randn(B, T, D_V, device=dev, generator=g)
+    lv = (torch.rand(B, T, device=dev, generator=g) * 2 - 1).view(-1, B * T)
+    la = (torch.rand(B, T, device=dev, generator=g) * 2 - 1).view(-1, B * T)
+    crit = CCCLoss(1)
+
+    def fwd_bwd():
+        with JF.compute_mode(cd):
+            vo, ao = model(fc(audio), video)
+            l1 = crit(vo.view(-1, vo.shape[0] * vo.shape[1]), lv)
+            l2 = crit(ao.view(-1, ao.shape[0] * ao.shape[1]), la)
+            loss = l1 + l2
+            loss.backward()
+        return loss
+
+    params = used_parameters(fwd_bwd, list(model.parameters()) + list(fc.parameters()))
+    opt = FusedSGD(params, lr=1e-4, momentum=0.9, dampening=0.0, weight_decay=1e-4,
+                   nesterov=True, shadow_dtype=cd if cd != torch.float32 else None)
+
+    def step():
+        opt.zero_grad()
+        loss = fwd_bwd()
+        if world > 1:
+            bucket = 16 << 20   # elements per all-reduce bucket
+            for off in range(0, opt.numel, bucket):
+                dist.all_reduce(opt.flat_g[off:off + bucket])
+        opt.step()
+        return loss
+
+    probe = GemmProbe((ops.dt(cd), True, True))
+    if not args.no_probe:
+        ops.set_launch_hook(probe)
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    probe.on = not args.no_probe
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    probe.on = False
+    last_loss = float(loss)
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    windows = B * world * args.steps
+    value = windows / elapsed
+
+    psum = probe.summary()
+    roofline = None
+    if psum:
+        achieved = psum["avg_flops"] / (psum["avg_ms"] * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "kernel": "gemm_kernel<bf16,Kmajor,Kmajor> (NT: all forward "
+                    "linears + attention scores)", "achieved": round(achieved, 1),
+                    "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                    "launches_per_step": psum["launches"] // args.steps,
+                    "avg_launch_us": round(psum["avg_ms"] * 1e3, 2),
+                    "avg_gflop_per_launch": round(psum["avg_flops"] / 1e9, 3)}
+    step_tf = step_flops(B, T) * world / (elapsed / args.steps) / 1e12
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(model_sd0, fc_sd0, args.cpu_batch, T)
+
+    if rank == 0:
+        out = {
+            "metric": "train windows/sec + CCC parity, B=64 T=300 A/V fusion, 1/2/4/8 MI355X",
+            "value": round(value, 2), "unit": "windows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.dtype, "data": "synthetic (N(0,1) features, U(-1,1) labels, "
+                                         "random-init weights)",
+            "config": {"workload": "configs[2]: FcLayer(1024,512) + Two_transformers(TRANSFORMER,"
+                                   "FC,H=1,L=1,vision_in_ft=2048) + 2x CCCLoss + SGD-nesterov",
+                       "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
+                       "D_a": D_A, "D_v": D_V, "parallelism": f"dp{world}"},
+            "roofline": roofline,
+            "step_mfma": {"algorithmic_tflop_per_step": round(step_flops(B, T) * world / 1e12, 4),
+                          "achieved_tflops": round(step_tf, 1),
+                          "frac_of_peak": round(step_tf / (PEAK_BF16_TFLOPS * world), 4)},
+            "cpu_baseline": cpu,
+            "final_loss": round(last_loss, 6),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

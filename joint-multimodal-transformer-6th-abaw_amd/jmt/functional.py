@@ -16,7 +16,6 @@ Layout conventions
 from __future__ import annotations
 
 import math
-import weakref
 from typing import Optional
 
 import torch
@@ -63,24 +62,22 @@ def _vec(dtype: torch.dtype) -> int:
 
 
 # ------------------------------------------------------------------------- weight shadows
-_shadows: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
-
-
 def weight_as(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
-    """fp32 parameter -> contiguous compute-dtype copy (cached by parameter identity+version)."""
+    """fp32 parameter -> contiguous compute-dtype copy, cached on the parameter itself and
+    re-cast only when the parameter's version / storage changes."""
     if w.dtype == dtype:
         return w if w.is_contiguous() else w.contiguous()
-    ent = _shadows.get(w)
+    ent = getattr(w, "_jmt_shadow", None)
     if ent is not None and ent[0] == w._version and ent[1] == dtype and ent[2] == w.data_ptr():
         return ent[3]
     t = ops.cast(w.detach(), dtype)
-    _shadows[w] = (w._version, dtype, w.data_ptr(), t)
+    w._jmt_shadow = (w._version, dtype, w.data_ptr(), t)
     return t
 
 
 def register_shadow(w: torch.Tensor, shadow: torch.Tensor):
     """Used by the fused optimizer, which rewrites `shadow` in the same kernel as `w`."""
-    _shadows[w] = (w._version, shadow.dtype, w.data_ptr(), shadow)
+    w._jmt_shadow = (w._version, shadow.dtype, w.data_ptr(), shadow)
 
 
 def _grad_buffer(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -109,7 +106,9 @@ class Rows:
         dims = [d for d in perm if x.shape[d] != 1]
         ok = all(x.stride(a) == x.stride(b) * x.shape[b] for a, b in zip(dims[:-1], dims[1:]))
         ld = x.stride(dims[-1]) if dims else max(x.shape[-1], 1)
-        if not ok or ld < x.shape[-1] or ld % _vec(x.dtype) or x.data_ptr() % 16:
+        # (a column vector F == 1 with ld == 1 is a dense vector: keep its row order)
+        if not ok or ld < x.shape[-1] or (ld % _vec(x.dtype) and x.shape[-1] > 1) or \
+                x.data_ptr() % 16:
             x = x.contiguous() if x.data_ptr() % 16 == 0 else x.clone()
             perm = lead
             ld = x.shape[-1]

@@ -37,6 +37,15 @@ def workspace(nbytes: int, device) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------------ GEMM
+_launch_hook = None
+
+
+def set_launch_hook(hook) -> None:
+    """hook(info: dict, launch: callable) -> result; used by bench.py to bracket launches of one
+    GEMM instance with HIP events on the launch stream.  None disables."""
+    global _launch_hook
+    _launch_hook = hook
+
 
 def auto_splits(M: int, N: int, K: int, batch: int, bk: int = 64) -> int:
     tiles = math.ceil(M / 128) * math.ceil(N / 128) * batch
@@ -88,7 +97,13 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
         ws = workspace(nbytes, device)
         d.workspace = ws.data_ptr()
         d.ws_bytes = nbytes
-    _lib.check(_lib.load().jmt_gemm(C.byref(d), stream()), "jmt_gemm")
+    launch = lambda: _lib.check(_lib.load().jmt_gemm(C.byref(d), stream()), "jmt_gemm")
+    if _launch_hook is not None:
+        _launch_hook({"ab_dtype": ab_dtype, "a_kmajor": bool(a_kmajor),
+                      "b_kmajor": bool(b_kmajor), "M": M, "N": N, "K": K,
+                      "batch": batch0 * batch1}, launch)
+    else:
+        launch()
     return ws   # keep alive until the launch is ordered (caching allocator is stream-ordered)
 
 

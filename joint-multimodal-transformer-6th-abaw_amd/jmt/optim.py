@@ -23,7 +23,12 @@ class FusedSGD:
         self.params: List[torch.nn.Parameter] = list(params)
         assert self.params, "no parameters"
         dev = self.params[0].device
-        n = sum(p.numel() for p in self.params)
+        # every parameter starts on a 256-B boundary (16-B aligned MFMA operand loads)
+        offs = []
+        n = 0
+        for p in self.params:
+            offs.append(n)
+            n += -(-p.numel() // 64) * 64
         self.numel = n
         self.lr, self.momentum, self.dampening = lr, momentum, dampening
         self.weight_decay, self.nesterov = weight_decay, nesterov
@@ -32,24 +37,20 @@ class FusedSGD:
         self.buf = torch.zeros(n, dtype=torch.float32, device=dev) if momentum else None
         self.shadow = (torch.empty(n, dtype=shadow_dtype, device=dev)
                        if shadow_dtype not in (None, torch.float32) else None)
-        off = 0
+        self.flat_p.zero_()
         self._gviews = []
         with torch.no_grad():
-            for p in self.params:
+            for p, off in zip(self.params, offs):
                 k = p.numel()
                 self.flat_p[off:off + k].copy_(p.detach().reshape(-1))
                 p.data = self.flat_p[off:off + k].view_as(p)
                 g = self.flat_g[off:off + k].view_as(p)
                 p.grad = g
                 self._gviews.append(g)
-                off += k
         if self.shadow is not None:
             ops.cast(self.flat_p, self.shadow.dtype, out=self.shadow)
-            off = 0
-            for p in self.params:
-                k = p.numel()
-                F.register_shadow(p, self.shadow[off:off + k].view_as(p))
-                off += k
+            for p, off in zip(self.params, offs):
+                F.register_shadow(p, self.shadow[off:off + p.numel()].view_as(p))
         self.first = True
 
     def zero_grad(self, set_to_none: bool = False):
