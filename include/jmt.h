@@ -76,6 +76,8 @@ typedef struct jmt_gemm_desc {
 
 int jmt_gemm(const jmt_gemm_desc* desc, void* stream);
 size_t jmt_gemm_workspace_bytes(int M, int N, int batch, int splits);
+/* development only: GEMM ablation flags (1 = skip MFMA, 2 = skip epilogue stores), 0 = off */
+void jmt_gemm_set_debug(int flags);
 
 /* ------------------------------------------------------------------ row-wise ops
  * Rows are `rows` vectors of length D at stride ld (elements). */

@@ -52,6 +52,8 @@ struct GemmParams {
   int c_dtype;
   int aux_dtype;
   int tiles_m, tiles_n;
+  int c_vec;                    // C (and aux) rows 16-B aligned for 16-B vector stores
+  int dbg;                      // development ablations: 1 skip MFMA, 2 skip epilogue stores
 };
 
 template <typename T> struct Vec { static constexpr int n = 16 / sizeof(T); };
@@ -153,6 +155,51 @@ __device__ __forceinline__ void stage_store(char* img, const uint4 (&r)[4]) {
   }
 }
 
+// LDS-DMA staging of one FULL K-tile (global_load_lds_dwordx4, 1 KiB per wave-instruction, no
+// VGPR round trip).  The LDS destination of a wave-instruction is linear (base + 16*lane), so the
+// bank swizzles of kmaj_off / mnmaj16_off are applied to the per-lane GLOBAL source address
+// (rule 21 of the CDNA guide).  Rows past the matrix edge are clamped to a valid row: their
+// products only reach discarded outputs.  4 instructions per wave per operand.
+template <typename T, bool KMAJ>
+__device__ __forceinline__ void glds_tile(char* img, const T* base, int64_t ld, int rows_lim,
+                                          int r0, int kloc) {
+  constexpr int V = Vec<T>::n;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const T* src;
+    char* dst;
+    if constexpr (KMAJ) {                      // image [128 rows][128 B]
+      const int row0 = 32 * w + 8 * i;
+      const int row = row0 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int gr = min(r0 + row, rows_lim - 1);
+      src = base + (int64_t)gr * ld + kloc + c * V;
+      dst = img + row0 * 128;
+    } else if constexpr (sizeof(T) == 2) {     // image [64 k][256 B], 32-B pairs swizzled by t(k)
+      const int k0 = 16 * w + 4 * i;
+      const int k = k0 + (lane >> 4);
+      const int cp = lane & 15;
+      const int t = (k & 3) | (((k >> 3) & 1) << 2);
+      const int c = ((((cp >> 1) ^ t)) << 1) | (cp & 1);
+      int gm = r0 + c * V;
+      if (gm >= rows_lim) gm = ((rows_lim - 1) / V) * V;
+      src = base + (int64_t)(kloc + k) * ld + gm;
+      dst = img + k0 * 256;
+    } else {                                   // f32 image [32 k][512 B]
+      const int k0 = 8 * w + 2 * i;
+      const int k = k0 + (lane >> 5);
+      int gm = r0 + (lane & 31) * V;
+      if (gm >= rows_lim) gm = ((rows_lim - 1) / V) * V;
+      src = base + (int64_t)(kloc + k) * ld + gm;
+      dst = img + k0 * 512;
+    }
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  }
+}
+
 // ------------------------------------------------------------------ fragment reads
 template <typename T> struct Frag16;
 template <> struct Frag16<__bf16> { typedef bf16x8 t; typedef bf16x4 h; };
@@ -246,7 +293,117 @@ __device__ __forceinline__ void c_addr(const GemmParams& p, int b0, int b1, void
 
 // ------------------------------------------------------------------ main kernel
 template <typename T, bool AK, bool BK>
-__global__ __launch_bounds__(GT) void gemm_kernel(GemmParams p) {
+__device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB, int wm, int wn,
+                                             f32x4 (&acc)[4][4]) {
+  if constexpr (sizeof(T) == 2) {
+    typedef typename Frag16<T>::t F;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      F fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag16<T, AK>(imgA, wm * 64 + i * 16, ks);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag16<T, BK>(imgB, wn * 64 + j * 16, ks);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
+    }
+  } else {
+#pragma unroll
+    for (int seg = 0; seg < 2; ++seg) {
+      f32x4 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag32<AK>(imgA, wm * 64 + i * 16, seg);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag32<BK>(imgB, wn * 64 + j * 16, seg);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0,
+                                                             0);
+    }
+  }
+}
+
+template <typename O> struct OutVec { static constexpr int n = 16 / sizeof(O); };
+
+struct Epi {
+  float alpha, beta;
+  const float* bias;
+  int bias_mode, relu, N;
+  int64_t ldc, ldaux;
+};
+
+// Epilogue of one output row chunk of VO = 16/sizeof(O) columns at (m, n); v[] = fp32
+// accumulators.  16-B vector accesses when the chunk is interior and aligned (vec).
+template <typename O>
+__device__ __forceinline__ void store_chunk(const Epi& e, O* cp, int64_t cbase, const O* aux,
+                                            int m, int n, float (&v)[16 / sizeof(O)], bool vec) {
+  constexpr int VO = 16 / sizeof(O);
+  const int64_t co = cbase + (int64_t)m * e.ldc + n;
+  const bool full = vec && (n + VO <= e.N);
+  const int nv = min(VO, e.N - n);
+  float add[VO];
+#pragma unroll
+  for (int i = 0; i < VO; ++i) add[i] = 0.f;
+  if (e.bias_mode == 1) {
+#pragma unroll
+    for (int i = 0; i < VO; ++i) add[i] = (i < nv) ? e.bias[n + i] : 0.f;
+  } else if (e.bias_mode == 2) {
+    const float bm = e.bias[m];
+#pragma unroll
+    for (int i = 0; i < VO; ++i) add[i] = bm;
+  }
+  if (e.beta != 0.f) {
+    O old[VO];
+    if (full) {
+      *(uint4*)old = *(const uint4*)(cp + co);
+    } else {
+#pragma unroll
+      for (int i = 0; i < VO; ++i) old[i] = (i < nv) ? cp[co + i] : from_f<O>(0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < VO; ++i) add[i] += e.beta * to_f(old[i]);
+  }
+  O out[VO];
+  if (aux) {
+    const int64_t ao = cbase + (int64_t)m * e.ldaux + n;
+    O av[VO];
+    if (full) {
+      *(uint4*)av = *(const uint4*)(aux + ao);
+    } else {
+#pragma unroll
+      for (int i = 0; i < VO; ++i) av[i] = (i < nv) ? aux[ao + i] : from_f<O>(0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < VO; ++i) {
+      float x = v[i] * e.alpha + add[i];
+      if (e.relu) x = fmaxf(x, 0.f);
+      out[i] = from_f<O>(to_f(av[i]) > 0.f ? x : 0.f);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < VO; ++i) {
+      float x = v[i] * e.alpha + add[i];
+      if (e.relu) x = fmaxf(x, 0.f);
+      out[i] = from_f<O>(x);
+    }
+  }
+  if (full) {
+    *(uint4*)(cp + co) = *(const uint4*)out;
+  } else {
+#pragma unroll
+    for (int i = 0; i < VO; ++i)
+      if (i < nv) cp[co + i] = out[i];
+  }
+}
+
+template <typename T, typename O, bool AK, bool BK>
+__global__ __launch_bounds__(GT, 2) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TILE_BYTES = 16384;     // one operand image per stage
   constexpr bool F32 = sizeof(T) == 4;
@@ -269,7 +426,9 @@ __global__ __launch_bounds__(GT) void gemm_kernel(GemmParams p) {
   const int m0 = tm * BMT, n0 = tn * BNT;
   const int kbeg = split * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
-  const int nk = (kend - kbeg + BKE - 1) / BKE;
+  const int klen = max(0, kend - kbeg);
+  const int nfull = klen / BKE;
+  const bool tail = (klen % BKE) != 0;
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -281,9 +440,32 @@ __global__ __launch_bounds__(GT) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[4], rb[4];
-  auto load = [&](int kt) {
+  auto issue = [&](int kt, int buf) {
     const int k0 = kbeg + kt * BKE;
+    int ka, kb;
+    const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, b0, b1, p.a_kseg, k0, ka);
+    const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, b0, b1, p.b_kseg, k0, kb);
+    char* base = smem + buf * 2 * TILE_BYTES;
+    glds_tile<T, AK>(base, A, p.lda, p.M, m0, ka);
+    glds_tile<T, BK>(base + TILE_BYTES, B, p.ldb, p.N, n0, kb);
+  };
+
+  if (nfull > 0) issue(0, 0);
+  for (int kt = 0; kt < nfull; ++kt) {
+    if (kt + 1 < nfull) {
+      issue(kt + 1, (kt + 1) & 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // tile kt landed (8 newer in flight)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();                        // ... for every wave of the block
+    const char* imgA = smem + (kt & 1) * 2 * TILE_BYTES;
+    if (!(p.dbg & 1)) compute_tile<T, AK, BK>(imgA, imgA + TILE_BYTES, wm, wn, acc);
+    __builtin_amdgcn_s_barrier();                        // buffer (kt&1) free for tile kt+2
+  }
+  if (tail) {   // trailing partial K-tile: masked register staging
+    uint4 ra[4], rb[4];
+    const int k0 = kbeg + nfull * BKE;
     int ka, kb;
     const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, b0, b1, p.a_kseg, k0, ka);
     const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, b0, b1, p.b_kseg, k0, kb);
@@ -291,95 +473,86 @@ __global__ __launch_bounds__(GT) void gemm_kernel(GemmParams p) {
     const int kb_lim = (p.b_mode == 2) ? min(p.b_kseg, kb + (kend - k0)) : kend;
     stage_load<T, AK>(ra, A, p.lda, p.M, m0, ka_lim, ka);
     stage_load<T, BK>(rb, B, p.ldb, p.N, n0, kb_lim, kb);
-  };
-  auto store = [&](int buf) {
-    char* base = smem + buf * 2 * TILE_BYTES;
+    char* base = smem + (nfull & 1) * 2 * TILE_BYTES;
     stage_store<T, AK>(base, ra);
     stage_store<T, BK>(base + TILE_BYTES, rb);
-  };
-
-  if (nk > 0) {
-    load(0);
-    store(0);
+    __syncthreads();
+    if (!(p.dbg & 1)) compute_tile<T, AK, BK>(base, base + TILE_BYTES, wm, wn, acc);
   }
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load(kt + 1);
-    const char* imgA = smem + (kt & 1) * 2 * TILE_BYTES;
-    const char* imgB = imgA + TILE_BYTES;
-    if constexpr (!F32) {
-      typedef typename Frag16<T>::t F;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        F fa[4], fb[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = read_frag16<T, AK>(imgA, wm * 64 + i * 16, ks);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = read_frag16<T, BK>(imgB, wn * 64 + j * 16, ks);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
-      }
-    } else {
-#pragma unroll
-      for (int seg = 0; seg < 2; ++seg) {
-        f32x4 fa[4], fb[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = read_frag32<AK>(imgA, wm * 64 + i * 16, seg);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = read_frag32<BK>(imgB, wn * 64 + j * 16, seg);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j],
-                                                               0, 0, 0);
-      }
-    }
-    if (kt + 1 < nk) store((kt + 1) & 1);
-    __syncthreads();
-  }
 
-  // ---- epilogue: C/D layout of 16x16 MFMA: col = lane&15, row = 4*(lane>>4) + r
-  if (p.splits > 1) {
+  // ---- epilogue through LDS, one 64-row half at a time: C/D layout of 16x16 MFMA is
+  //      col = lane&15, row = 4*(lane>>4) + r; the store pass writes 16-B row chunks.
+  constexpr int CLD = 132;                  // padded fp32 row of the staged half tile
+  float* ct = (float*)smem;
+  const bool partial = p.splits > 1;
+  O* cp;
+  int64_t cbase;
+  const void* ap = partial ? nullptr : p.aux;
+  bool vec;
+  if (partial) {
     const int nb = p.batch0 * p.batch1;
-    float* ws = p.ws + ((int64_t)split * nb + b) * (int64_t)p.M * p.N;
+    cp = (O*)(p.ws + ((int64_t)split * nb + b) * (int64_t)p.M * p.N);
+    cbase = 0;
+    vec = (p.N % 4) == 0;
+  } else {
+    if (p.c_mode == 1) {
+      cp = (O*)p.c_ptr[b0];
+      cbase = (int64_t)b1 * p.sC1;
+    } else {
+      cp = (O*)p.c_ptr[0];
+      cbase = (int64_t)b0 * p.sC0 + (int64_t)b1 * p.sC1;
+    }
+    vec = p.c_vec != 0;
+  }
+  if (p.dbg & 2) {
+    float sum = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
-          if (m < p.M && n < p.N) ws[(int64_t)m * p.N + n] = acc[i][j][r];
-        }
-      }
+      for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sum == 12345.678f) ((float*)cp)[0] = sum;   // keep acc live
     return;
   }
-  void* cp;
-  int64_t cbase, abase;
-  const void* ap;
-  c_addr(p, b0, b1, cp, cbase, ap, abase);
+  Epi ep;
+  ep.alpha = p.alpha; ep.beta = p.beta; ep.bias = p.bias; ep.bias_mode = p.bias_mode;
+  ep.relu = p.relu; ep.N = p.N; ep.ldc = p.ldc; ep.ldaux = p.ldaux;
+  if (partial) {   // raw partial sums: no epilogue ops, row stride N
+    ep.alpha = 1.f; ep.beta = 0.f; ep.bias_mode = 0; ep.relu = 0; ep.ldc = p.N;
+  }
+  const O* auxp = (const O*)ap;
+  constexpr int VO = OutVec<O>::n;
+  constexpr int CPR = BNT / VO;                 // chunks per 128-col row
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
-        if (m < p.M && n < p.N) {
-          const int64_t co = cbase + (int64_t)m * p.ldc + n;
-          const int64_t ao = abase + (int64_t)m * p.ldaux + n;
-          const float v = epi_value(p, acc[i][j][r], m, n, cp, co, ap, ao);
-          st_dyn(cp, co, p.c_dtype, v);
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ct[(i * 16 + 4 * (lane >> 4) + r) * CLD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int it = 0; it < 64 * CPR / GT; ++it) {
+      const int id = threadIdx.x + GT * it;
+      const int rr = id / CPR, cc = (id % CPR) * VO;
+      const int m = m0 + 64 * h + rr, n = n0 + cc;
+      if (m < p.M && n < p.N) {
+        float v[VO];
+        const float* src = ct + rr * CLD + cc;
+#pragma unroll
+        for (int e = 0; e < VO; e += 4) {
+          const float4 t = *(const float4*)(src + e);
+          v[e] = t.x; v[e + 1] = t.y; v[e + 2] = t.z; v[e + 3] = t.w;
         }
+        store_chunk<O>(ep, cp, cbase, auxp, m, n, v, vec);
       }
     }
+    __syncthreads();
+  }
 }
 
 // split-K reduction + epilogue: one thread per output element (vector of 4 along n when possible)
@@ -405,18 +578,27 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   }
 }
 
+template <typename T, typename O>
+static void launch_to(const GemmParams& p, int ak, int bk, dim3 grid, hipStream_t st) {
+  const size_t lds = 4 * 16384;
+  if (ak && bk) hipLaunchKernelGGL((gemm_kernel<T, O, true, true>), grid, dim3(GT), lds, st, p);
+  else if (ak && !bk) hipLaunchKernelGGL((gemm_kernel<T, O, true, false>), grid, dim3(GT), lds, st, p);
+  else if (!ak && bk) hipLaunchKernelGGL((gemm_kernel<T, O, false, true>), grid, dim3(GT), lds, st, p);
+  else hipLaunchKernelGGL((gemm_kernel<T, O, false, false>), grid, dim3(GT), lds, st, p);
+}
+
 template <typename T>
 static void launch_t(const GemmParams& p, int ak, int bk, dim3 grid, hipStream_t st) {
-  const size_t lds = 4 * 16384;
-  if (ak && bk) hipLaunchKernelGGL((gemm_kernel<T, true, true>), grid, dim3(GT), lds, st, p);
-  else if (ak && !bk) hipLaunchKernelGGL((gemm_kernel<T, true, false>), grid, dim3(GT), lds, st, p);
-  else if (!ak && bk) hipLaunchKernelGGL((gemm_kernel<T, false, true>), grid, dim3(GT), lds, st, p);
-  else hipLaunchKernelGGL((gemm_kernel<T, false, false>), grid, dim3(GT), lds, st, p);
+  if (p.splits > 1 || p.c_dtype == JMT_F32) launch_to<T, float>(p, ak, bk, grid, st);
+  else launch_to<T, T>(p, ak, bk, grid, st);
 }
 
 }  // namespace jmt
 
 using namespace jmt;
+
+static int g_gemm_dbg = 0;
+extern "C" void jmt_gemm_set_debug(int flags) { g_gemm_dbg = flags; }
 
 extern "C" size_t jmt_gemm_workspace_bytes(int M, int N, int batch, int splits) {
   if (splits <= 1) return 0;
@@ -429,6 +611,8 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   JMT_CHECK_ARG(dt == JMT_F32 || dt == JMT_BF16 || dt == JMT_F16, "jmt_gemm: bad ab_dtype %d", dt);
   JMT_CHECK_ARG(d->c_dtype == JMT_F32 || d->c_dtype == dt, "jmt_gemm: c_dtype must be f32 or ab");
   JMT_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "jmt_gemm: negative size");
+  JMT_CHECK_ARG(d->aux == nullptr || d->aux_dtype == d->c_dtype,
+                "jmt_gemm: aux (ReLU mask) must have the output dtype");
   if (d->M == 0 || d->N == 0) return JMT_OK;
   const int batch0 = d->batch0 < 1 ? 1 : d->batch0;
   const int batch1 = d->batch1 < 1 ? 1 : d->batch1;
@@ -475,6 +659,15 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   p.aux_dtype = d->aux_dtype;
   p.tiles_m = (d->M + BMT - 1) / BMT;
   p.tiles_n = (d->N + BNT - 1) / BNT;
+  p.dbg = g_gemm_dbg;
+  {
+    const int ces = dtype_size(d->c_dtype);
+    const int VO = 16 / ces;
+    bool cv = d->ldc % VO == 0 && d->sC0 % VO == 0 && d->sC1 % VO == 0;
+    for (int i = 0; i < d->n_c; ++i) cv = cv && (((uintptr_t)d->c[i] & 15) == 0);
+    if (d->aux) cv = cv && (((uintptr_t)d->aux & 15) == 0) && d->ldaux % VO == 0;
+    p.c_vec = cv ? 1 : 0;
+  }
 
   int splits = d->splits < 1 ? 1 : d->splits;
   // each split must own whole K-tiles, and a K-concat segment boundary must not cut a tile

@@ -106,83 +106,190 @@ __global__ __launch_bounds__(RB) void ln_fwd_kernel(int64_t rows, int D, const T
   }
 }
 
-constexpr int LN_ROWS_PER_BLOCK = 64;   // 16 rows per wave
+constexpr int LN_ROWS_PER_BLOCK = 128;   // 32 rows per wave
 
+// 4-element vector loads/stores (8 B for 16-bit types, 16 B for f32); rows are 4-aligned
+template <typename T> struct V4;
+template <> struct V4<float> {
+  static __device__ __forceinline__ void ld(const float* p, float (&v)[4]) {
+    const float4 t = *(const float4*)p;
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+  static __device__ __forceinline__ void st(float* p, const float (&v)[4]) {
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <typename H> struct V4h {
+  static __device__ __forceinline__ void ld(const H* p, float (&v)[4]) {
+    const uint2 t = *(const uint2*)p;
+    const H* h = (const H*)&t;
+    v[0] = (float)h[0]; v[1] = (float)h[1]; v[2] = (float)h[2]; v[3] = (float)h[3];
+  }
+  static __device__ __forceinline__ void st(H* p, const float (&v)[4]) {
+    H h[4] = {(H)v[0], (H)v[1], (H)v[2], (H)v[3]};
+    *(uint2*)p = *(const uint2*)h;
+  }
+};
+template <> struct V4<__bf16> : V4h<__bf16> {};
+template <> struct V4<_Float16> : V4h<_Float16> {};
+
+// NV = D / 256: lane owns elements 4*(lane + 64 j) .. +3, j < NV
+template <typename TI, typename TG, typename TD, int NV>
+__global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* x, int64_t ldx,
+                                                        const TI* rr, int64_t ldr, const TG* dy,
+                                                        int64_t lddy, const float* mean,
+                                                        const float* rstd, const float* gamma,
+                                                        TD* dx, int64_t lddx, float* partials) {
+  constexpr int D = NV * 256;
+  __shared__ float red[4][2][D];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  float pg[NV][4], pb[NV][4], gm[NV][4];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float4 g4 = *(const float4*)(gamma + 4 * (lane + 64 * j));
+    gm[j][0] = g4.x; gm[j][1] = g4.y; gm[j][2] = g4.z; gm[j][3] = g4.w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pg[j][e] = pb[j][e] = 0.f;
+  }
+  const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK;
+  for (int i = w; i < LN_ROWS_PER_BLOCK; i += 4) {
+    const int64_t r = rbeg + i;
+    if (r >= rows) break;
+    const float mu = mean[r], rs = rstd[r];
+    float xh[NV][4], gd[NV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      float xv[4], gv[4];
+      V4<TI>::ld(x + r * ldx + c, xv);
+      if (rr) {
+        float rv[4];
+        V4<TI>::ld(rr + r * ldr + c, rv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[e] += rv[e];
+      }
+      V4<TG>::ld(dy + r * lddy + c, gv);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[j][e] = (xv[e] - mu) * rs;
+        pg[j][e] += gv[e] * xh[j][e];
+        pb[j][e] += gv[e];
+        gd[j][e] = gv[e] * gm[j][e];
+        s1 += gd[j][e];
+        s2 += gd[j][e] * xh[j][e];
+      }
+    }
+    s1 = wave_sum(s1) * (1.f / D);
+    s2 = wave_sum(s2) * (1.f / D);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = rs * (gd[j][e] - s1 - xh[j][e] * s2);
+      V4<TD>::st(dx + r * lddx + 4 * (lane + 64 * j), o);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[w][0][4 * (lane + 64 * j) + e] = pg[j][e];
+      red[w][1][4 * (lane + 64 * j) + e] = pb[j][e];
+    }
+  __syncthreads();
+  float* out = partials + (int64_t)blockIdx.x * 2 * D;
+  for (int c = threadIdx.x; c < 2 * D; c += RB) {
+    const int h = c / D, cc = c - h * D;
+    out[c] = red[0][h][cc] + red[1][h][cc] + red[2][h][cc] + red[3][h][cc];
+  }
+}
+
+// generic fallback (any D <= 2048): one element per lane-stride
 template <typename TI, typename TG, typename TD>
 __global__ __launch_bounds__(RB) void ln_bwd_kernel(int64_t rows, int D, const TI* x, int64_t ldx,
                                                     const TI* rr, int64_t ldr, const TG* dy,
                                                     int64_t lddy, const float* mean,
                                                     const float* rstd, const float* gamma, TD* dx,
                                                     int64_t lddx, float* partials) {
-  constexpr int MAXC = 32;
-  __shared__ float red[4][2][64];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  float pg[MAXC], pb[MAXC];
-#pragma unroll
-  for (int j = 0; j < MAXC; ++j) pg[j] = pb[j] = 0.f;
+  __shared__ float red[4][64];
   const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK;
   for (int i = w; i < LN_ROWS_PER_BLOCK; i += 4) {
     const int64_t r = rbeg + i;
     if (r >= rows) break;
     const float mu = mean[r], rs = rstd[r];
-    const TI* xr = x + r * ldx;
-    const TI* res = rr ? rr + r * ldr : nullptr;
-    const TG* gr = dy + r * lddy;
-    float xh[MAXC], gd[MAXC];
     float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int j = 0; j < MAXC; ++j) {
-      const int c = lane + 64 * j;
-      xh[j] = 0.f;
-      gd[j] = 0.f;
-      if (c < D) {
-        float t = to_f(xr[c]);
-        if (res) t += to_f(res[c]);
-        xh[j] = (t - mu) * rs;
-        const float g = to_f(gr[c]);
-        pg[j] += g * xh[j];
-        pb[j] += g;
-        gd[j] = g * gamma[c];
-        s1 += gd[j];
-        s2 += gd[j] * xh[j];
-      }
+    for (int c = lane; c < D; c += 64) {
+      float t = to_f(x[r * ldx + c]);
+      if (rr) t += to_f(rr[r * ldr + c]);
+      const float xh = (t - mu) * rs;
+      const float gd = to_f(dy[r * lddy + c]) * gamma[c];
+      s1 += gd;
+      s2 += gd * xh;
     }
     s1 = wave_sum(s1) / (float)D;
     s2 = wave_sum(s2) / (float)D;
-    TD* dr = dx + r * lddx;
-#pragma unroll
-    for (int j = 0; j < MAXC; ++j) {
-      const int c = lane + 64 * j;
-      if (c < D) dr[c] = from_f<TD>(rs * (gd[j] - s1 - xh[j] * s2));
+    for (int c = lane; c < D; c += 64) {
+      float t = to_f(x[r * ldx + c]);
+      if (rr) t += to_f(rr[r * ldr + c]);
+      const float xh = (t - mu) * rs;
+      const float gd = to_f(dy[r * lddy + c]) * gamma[c];
+      dx[r * lddx + c] = from_f<TD>(rs * (gd - s1 - xh * s2));
     }
   }
-  // block-reduce the per-wave column partials -> partials[blk][2][D]
+  // column partials: each wave sums its columns over the block's rows
   float* out = partials + (int64_t)blockIdx.x * 2 * D;
-#pragma unroll
-  for (int j = 0; j < MAXC; ++j) {
-    const int c = lane + 64 * j;
-    if (64 * j >= D) break;
-    red[w][0][lane] = pg[j];
-    red[w][1][lane] = pb[j];
-    __syncthreads();
-    if (w == 0 && c < D) {
-      out[c] = red[0][0][lane] + red[1][0][lane] + red[2][0][lane] + red[3][0][lane];
-      out[D + c] = red[0][1][lane] + red[1][1][lane] + red[2][1][lane] + red[3][1][lane];
+  for (int c0 = 0; c0 < D; c0 += 64) {
+    const int c = c0 + lane;
+    float pg = 0.f, pb = 0.f;
+    if (c < D) {
+      for (int i = w; i < LN_ROWS_PER_BLOCK; i += 4) {
+        const int64_t r = rbeg + i;
+        if (r >= rows) break;
+        float t = to_f(x[r * ldx + c]);
+        if (rr) t += to_f(rr[r * ldr + c]);
+        const float g = to_f(dy[r * lddy + c]);
+        pg += g * (t - mean[r]) * rstd[r];
+        pb += g;
+      }
     }
+    red[w][lane] = pg;
+    __syncthreads();
+    if (w == 0 && c < D) out[c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    __syncthreads();
+    red[w][lane] = pb;
+    __syncthreads();
+    if (w == 0 && c < D) out[D + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
     __syncthreads();
   }
 }
 
 // sum partial slabs: out[c] (+)= sum_b partials[b*stride + off + c]
+// block = 64 columns x 4 slab groups; slabs strided over the groups, reduced through LDS.
 __global__ __launch_bounds__(RB) void slab_reduce_kernel(int nblk, int D, const float* partials,
                                                          int64_t stride, int64_t off, float* out,
                                                          int beta_acc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partials[(int64_t)b * stride + off + c];
-  out[c] = beta_acc ? out[c] + s : s;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < D) {
+    int b = g;
+    for (; b + 4 < nblk; b += 8) {
+      s0 += partials[(int64_t)b * stride + off + c];
+      s1 += partials[(int64_t)(b + 4) * stride + off + c];
+    }
+    for (; b < nblk; b += 4) s0 += partials[(int64_t)b * stride + off + c];
+  }
+  red[g][lane] = s0 + s1;
+  __syncthreads();
+  if (g == 0 && c < D) {
+    const float s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[c] = beta_acc ? out[c] + s : s;
+  }
 }
 
 // ------------------------------------------------------------------ softmax
@@ -225,7 +332,39 @@ __global__ __launch_bounds__(RB) void softmax_bwd_kernel(int64_t rows, int n, co
 }
 
 // ------------------------------------------------------------------ column sums (bias grad)
-constexpr int CS_ROWS = 128;
+constexpr int CS_ROWS = 256;
+
+// N % 4 == 0: block = 64 columns (16 quads) x 16 row lanes over CS_ROWS rows
+template <typename T>
+__global__ __launch_bounds__(RB) void colsum_vec_kernel(int64_t rows, int N, const T* dy,
+                                                        int64_t ld, float* partials) {
+  __shared__ float red[16][64];
+  const int q = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c = blockIdx.y * 64 + 4 * q;
+  const int64_t r0 = (int64_t)blockIdx.x * CS_ROWS;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+#pragma unroll 4
+    for (int i = rl; i < CS_ROWS; i += 16) {
+      const int64_t r = r0 + i;
+      if (r >= rows) break;
+      float v[4];
+      V4<T>::ld(dy + r * ld + c, v);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[rl][4 * q + e] = acc[e];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int cc = blockIdx.y * 64 + threadIdx.x;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[i][threadIdx.x];
+    if (cc < N) partials[(int64_t)blockIdx.x * N + cc] = s;
+  }
+}
 
 template <typename T>
 __global__ __launch_bounds__(RB) void colsum_kernel(int64_t rows, int N, const T* dy, int64_t ld,
@@ -327,12 +466,24 @@ extern "C" int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, 
                 "jmt_layernorm_bwd: null pointer");
   hipStream_t st = as_stream(stream);
   const int nblk = jmt_layernorm_bwd_blocks(rows);
+  const bool vec = (D % 256 == 0) && (ldx % 4 == 0) && (lddy % 4 == 0) && (lddx % 4 == 0) &&
+                   (!r || ldr % 4 == 0) && ((uintptr_t)gamma % 16 == 0);
+#define JMT_LNB_VEC(NV)                                                                     \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV>), dim3(nblk), dim3(RB), 0, st, rows, \
+                     (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd, \
+                     gamma, (TD*)dx, lddx, partials)
   JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_dy, TG, JMT_DISPATCH1(dt_dx, TD,
-      hipLaunchKernelGGL((ln_bwd_kernel<TI, TG, TD>), dim3(nblk), dim3(RB), 0, st, rows, D,
-                         (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd,
-                         gamma, (TD*)dx, lddx, partials))));
+      if (vec && D == 512) { JMT_LNB_VEC(2); }
+      else if (vec && D == 768) { JMT_LNB_VEC(3); }
+      else if (vec && D == 1024) { JMT_LNB_VEC(4); }
+      else {
+        hipLaunchKernelGGL((ln_bwd_kernel<TI, TG, TD>), dim3(nblk), dim3(RB), 0, st, rows, D,
+                           (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd,
+                           gamma, (TD*)dx, lddx, partials);
+      })));
+#undef JMT_LNB_VEC
   JMT_LAUNCH_CHECK("jmt_layernorm_bwd");
-  const unsigned g = (unsigned)((D + RB - 1) / RB);
+  const unsigned g = (unsigned)((D + 63) / 64);
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(g), dim3(RB), 0, st, nblk, D, partials,
                      (int64_t)2 * D, (int64_t)0, dgamma, beta_acc);
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(g), dim3(RB), 0, st, nblk, D, partials,
@@ -377,10 +528,15 @@ extern "C" int jmt_colsum(int dt, int64_t rows, int N, const void* dy, int64_t l
     if (!beta_acc) (void)hipMemsetAsync(db, 0, sizeof(float) * N, st);
     return JMT_OK;
   }
+  const bool vec = (N % 4 == 0) && (ld % 4 == 0) && ((uintptr_t)dy % 8 == 0);
   JMT_DISPATCH1(dt, T,
-      hipLaunchKernelGGL((colsum_kernel<T>), dim3(nblk, (N + RB - 1) / RB), dim3(RB), 0, st, rows,
-                         N, (const T*)dy, ld, partials));
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((N + RB - 1) / RB), dim3(RB), 0, st, nblk, N,
+      if (vec)
+        hipLaunchKernelGGL((colsum_vec_kernel<T>), dim3(nblk, (N + 63) / 64), dim3(RB), 0, st,
+                           rows, N, (const T*)dy, ld, partials);
+      else
+        hipLaunchKernelGGL((colsum_kernel<T>), dim3(nblk, (N + RB - 1) / RB), dim3(RB), 0, st,
+                           rows, N, (const T*)dy, ld, partials));
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((N + 63) / 64), dim3(RB), 0, st, nblk, N,
                      partials, (int64_t)N, (int64_t)0, db, beta_acc);
   JMT_LAUNCH_CHECK("jmt_colsum");
   return JMT_OK;

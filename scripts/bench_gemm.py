@@ -1,0 +1,75 @@
+"""GEMM micro-benchmark on the JMT step's shapes (bf16), with optional ablations:
+    python scripts/bench_gemm.py [--dbg 0|1|2|3] [--reps 50]
+Prints per shape: µs/launch, TFLOP/s, and the algorithmic-bytes GB/s."""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "joint-multimodal-transformer-6th-abaw_amd")]
+
+import torch  # noqa: E402
+
+from jmt import _lib, ops  # noqa: E402
+from jmt._lib import BF16, F32  # noqa: E402
+
+# (name, M, N, K, a_kmajor, b_kmajor, batch, c_dtype, splits)
+SHAPES = [
+    ("fwd 19200x512x512 NT", 19200, 512, 512, True, True, 1, BF16, 1),
+    ("fwd qkv 19200x1536x512 NT", 19200, 1536, 512, True, True, 1, BF16, 1),
+    ("fwd out1 19200x1024x3072 NT", 19200, 1024, 3072, True, True, 1, BF16, 1),
+    ("dgrad 19200x512x512 NN", 19200, 512, 512, True, False, 1, BF16, 1),
+    ("wgrad 512x512x19200 TN", 512, 512, 19200, False, False, 1, F32, None),
+    ("attn S 300x300x512 b64 NT", 300, 300, 512, True, True, 64, F32, 1),
+    ("attn PV 300x512x300 b64 NN", 300, 512, 300, True, False, 64, BF16, 1),
+    ("attn dK 300x512x300 b64 TN", 300, 512, 300, False, False, 64, BF16, 1),
+]
+
+
+def run(reps, dbg):
+    lib = _lib.load()
+    lib.jmt_gemm_set_debug(dbg)
+    dev = "cuda"
+    out = []
+    for name, M, N, K, ak, bk, batch, cdt, splits in SHAPES:
+        a = torch.randn(batch, M * K, device=dev).bfloat16()
+        b = torch.randn(batch, N * K, device=dev).bfloat16()
+        c = torch.empty(batch, M * N, device=dev,
+                        dtype=torch.float32 if cdt == F32 else torch.bfloat16)
+        r8 = lambda v: -(-v // 8) * 8
+        lda = r8(K) if ak else r8(M)
+        ldb = r8(K) if bk else r8(N)
+        a = torch.randn(batch, (M if ak else K) * lda, device=dev).bfloat16()
+        b = torch.randn(batch, (N if bk else K) * ldb, device=dev).bfloat16()
+        kw = dict(M=M, N=N, K=K, ab_dtype=BF16, c_dtype=cdt, a=[a.data_ptr()], lda=lda,
+                  a_kmajor=ak, b=[b.data_ptr()], ldb=ldb, b_kmajor=bk, c=[c.data_ptr()], ldc=N,
+                  batch0=batch, sA=(a.shape[1], 0), sB=(b.shape[1], 0), sC=(M * N, 0), splits=splits,
+                  device=dev)
+        for _ in range(3):
+            ops.gemm(**kw)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            ops.gemm(**kw)
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / reps * 1e3
+        fl = 2.0 * M * N * K * batch
+        by = (M * K + N * K) * 2 * batch + M * N * c.element_size() * batch
+        r = {"shape": name, "dbg": dbg, "us": round(us, 2), "tflops": round(fl / us / 1e6, 1),
+             "gbs": round(by / us / 1e3, 1)}
+        out.append(r)
+        print(json.dumps(r), flush=True)
+    lib.jmt_gemm_set_debug(0)
+    return out
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--dbg", type=int, nargs="*", default=[0])
+    args = ap.parse_args()
+    for d in args.dbg:
+        run(args.reps, d)

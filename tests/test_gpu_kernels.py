@@ -90,12 +90,12 @@ def test_gemm_epilogues_and_splitk(dt):
         ref = 0.5 * base + biasr[:, None] + C0
         assert (C - ref).abs().max().item() <= _tol(dt, K) * ref.abs().max().item()
         # aux mask (ReLU backward): zero where aux <= 0
-        aux = torch.randn(M, N, device=DEV, generator=g).to(TD[dt])
+        aux = torch.randn(M, N, device=DEV, generator=g)      # the mask has the output dtype
         C = torch.empty(M, N, device=DEV)
         ops.gemm(M=M, N=N, K=K, ab_dtype=dt, c_dtype=F32, a=[A.data_ptr()], lda=lda, a_kmajor=True,
                  b=[Bs.data_ptr()], ldb=ldb, b_kmajor=True, c=[C.data_ptr()], ldc=N, aux=aux,
                  ldaux=N, splits=splits, device=DEV)
-        ref = torch.where(aux.float() > 0, base, torch.zeros_like(base))
+        ref = torch.where(aux > 0, base, torch.zeros_like(base))
         assert (C - ref).abs().max().item() <= _tol(dt, K) * base.abs().max().item()
 
 
