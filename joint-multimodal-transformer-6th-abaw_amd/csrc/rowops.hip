@@ -106,7 +106,7 @@ __global__ __launch_bounds__(RB) void ln_fwd_kernel(int64_t rows, int D, const T
   }
 }
 
-constexpr int LN_ROWS_PER_BLOCK = 128;   // 32 rows per wave
+constexpr int LN_ROWS_PER_BLOCK = 32;    // 8 rows per wave (600 blocks at B*T = 19200)
 
 // 4-element vector loads/stores (8 B for 16-bit types, 16 B for f32); rows are 4-aligned
 template <typename T> struct V4;

@@ -48,11 +48,14 @@ def set_launch_hook(hook) -> None:
 
 
 def auto_splits(M: int, N: int, K: int, batch: int, bk: int = 64) -> int:
+    """Split-K factor: aim at >= 512 blocks (2 per CU) while keeping >= 8 K-tiles per split."""
     tiles = math.ceil(M / 128) * math.ceil(N / 128) * batch
-    if tiles >= 192 or K < 4 * bk:
+    if tiles >= 512:
         return 1
-    want = math.ceil(512 / tiles)
-    return max(1, min(want, K // (2 * bk), 32))
+    max_by_k = K // (8 * bk)
+    if max_by_k < 2:
+        return 1
+    return max(1, min(math.ceil(512 / tiles), max_by_k, 32))
 
 
 def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
