@@ -523,6 +523,22 @@ __global__ __launch_bounds__(GT, 2) void gemm_kernel(GemmParams p) {
   const O* auxp = (const O*)ap;
   constexpr int VO = OutVec<O>::n;
   constexpr int CPR = BNT / VO;                 // chunks per 128-col row
+  constexpr int RPI = GT / CPR;                 // rows covered per pass
+  constexpr int NIT = 64 / RPI;                 // passes per 64-row half
+  // each thread owns ONE column chunk for the whole epilogue (GT is a multiple of CPR)
+  const int cc = (threadIdx.x % CPR) * VO;
+  const int r_in = threadIdx.x / CPR;
+  const int n = n0 + cc;
+  const bool col_ok = n < p.N;
+  const int nv = min(VO, p.N - n);
+  const bool full = vec && (n + VO <= p.N);
+  float bvec[VO];
+#pragma unroll
+  for (int i = 0; i < VO; ++i) bvec[i] = 0.f;
+  if (ep.bias_mode == 1 && col_ok) {
+#pragma unroll
+    for (int i = 0; i < VO; ++i) bvec[i] = (i < nv) ? ep.bias[n + i] : 0.f;
+  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (wm == h) {
@@ -535,20 +551,59 @@ __global__ __launch_bounds__(GT, 2) void gemm_kernel(GemmParams p) {
             ct[(i * 16 + 4 * (lane >> 4) + r) * CLD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
     }
     __syncthreads();
-#pragma unroll 1
-    for (int it = 0; it < 64 * CPR / GT; ++it) {
-      const int id = threadIdx.x + GT * it;
-      const int rr = id / CPR, cc = (id % CPR) * VO;
-      const int m = m0 + 64 * h + rr, n = n0 + cc;
-      if (m < p.M && n < p.N) {
-        float v[VO];
-        const float* src = ct + rr * CLD + cc;
+    // phase 1: LDS reads + every global load of the pass (C_old, aux) issued back to back
+    float v[NIT][VO];
+    O oldv[NIT][VO];
+    O auxv[NIT][VO];
 #pragma unroll
-        for (int e = 0; e < VO; e += 4) {
-          const float4 t = *(const float4*)(src + e);
-          v[e] = t.x; v[e + 1] = t.y; v[e + 2] = t.z; v[e + 3] = t.w;
-        }
-        store_chunk<O>(ep, cp, cbase, auxp, m, n, v, vec);
+    for (int it = 0; it < NIT; ++it) {
+      const int rr = r_in + RPI * it;
+      const float* src = ct + rr * CLD + cc;
+#pragma unroll
+      for (int e = 0; e < VO; e += 4) {
+        const float4 t = *(const float4*)(src + e);
+        v[it][e] = t.x; v[it][e + 1] = t.y; v[it][e + 2] = t.z; v[it][e + 3] = t.w;
+      }
+      const int m = m0 + 64 * h + rr;
+      const bool ok = col_ok && m < p.M;
+      const int64_t co = cbase + (int64_t)m * ep.ldc + n;
+      const int64_t ao = cbase + (int64_t)m * ep.ldaux + n;
+      if (ep.beta != 0.f) {
+        if (ok && full) *(uint4*)oldv[it] = *(const uint4*)(cp + co);
+        else
+#pragma unroll
+          for (int i = 0; i < VO; ++i) oldv[it][i] = (ok && i < nv) ? cp[co + i] : from_f<O>(0.f);
+      }
+      if (auxp) {
+        if (ok && full) *(uint4*)auxv[it] = *(const uint4*)(auxp + ao);
+        else
+#pragma unroll
+          for (int i = 0; i < VO; ++i) auxv[it][i] = (ok && i < nv) ? auxp[ao + i] : from_f<O>(0.f);
+      }
+    }
+    // phase 2: epilogue math + 16-B stores
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int rr = r_in + RPI * it;
+      const int m = m0 + 64 * h + rr;
+      if (!(col_ok && m < p.M)) continue;
+      const float bm = (ep.bias_mode == 2) ? ep.bias[m] : 0.f;
+      O out[VO];
+#pragma unroll
+      for (int i = 0; i < VO; ++i) {
+        float x = v[it][i] * ep.alpha + bvec[i] + bm;
+        if (ep.beta != 0.f) x += ep.beta * to_f(oldv[it][i]);
+        if (ep.relu) x = fmaxf(x, 0.f);
+        if (auxp && !(to_f(auxv[it][i]) > 0.f)) x = 0.f;
+        out[i] = from_f<O>(x);
+      }
+      const int64_t co = cbase + (int64_t)m * ep.ldc + n;
+      if (full) {
+        *(uint4*)(cp + co) = *(const uint4*)out;
+      } else {
+#pragma unroll
+        for (int i = 0; i < VO; ++i)
+          if (i < nv) cp[co + i] = out[i];
       }
     }
     __syncthreads();

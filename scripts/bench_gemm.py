@@ -70,6 +70,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--dbg", type=int, nargs="*", default=[0])
+    ap.add_argument("--only", default="", help="substring filter on shape names")
     args = ap.parse_args()
+    if args.only:
+        SHAPES[:] = [s for s in SHAPES if args.only in s[0]]
     for d in args.dbg:
         run(args.reps, d)
