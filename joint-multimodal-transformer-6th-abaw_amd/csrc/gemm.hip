@@ -73,20 +73,23 @@ __device__ __forceinline__ const T* operand_base(const void* const* ptrs, int mo
   return p + (mode == 1 ? 0 : (int64_t)b0 * s0) + (int64_t)b1 * s1;
 }
 
-// Staging: each thread moves 4 x 16-byte chunks per operand per K-tile.
-// K-major image: 128 rows x 8 chunks; MN-major image: BK rows x (BMT*sizeof(T)/16) chunks.
-template <typename T, bool KMAJ>
-__device__ __forceinline__ void stage_load(uint4 (&r)[4], const T* base, int64_t ld, int rows_lim,
-                                           int r0, int k_lim, int kloc) {
+// K-tile geometry: KB = bytes per operand row of one K-tile (128 or 64), BKE = KB / sizeof(T)
+// K elements.  Register staging (used only for a trailing partial K-tile): each thread moves
+// KB/32 chunks of 16 B per operand.  K-major image: 128 rows x KB/16 chunks; MN-major image:
+// BKE rows x (128*sizeof(T)/16) chunks.
+template <typename T, bool KMAJ, int KB>
+__device__ __forceinline__ void stage_load(uint4 (&r)[KB / 32], const T* base, int64_t ld,
+                                           int rows_lim, int r0, int k_lim, int kloc) {
   constexpr int V = Vec<T>::n;
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < KB / 32; ++i) {
     const int id = tid + GT * i;
     int row, kk;
     if constexpr (KMAJ) {
-      row = id >> 3;
-      kk = (id & 7) * V;
+      constexpr int CPRK = KB / 16;
+      row = id / CPRK;
+      kk = (id % CPRK) * V;
     } else {
       constexpr int CPR = BMT * (int)sizeof(T) / 16;   // chunks per image row
       kk = id / CPR;
@@ -124,9 +127,15 @@ __device__ __forceinline__ void stage_load(uint4 (&r)[4], const T* base, int64_t
   }
 }
 
-// byte offset of 16-B chunk `c` of image row `row` in a K-major image (128-B rows)
-__device__ __forceinline__ int kmaj_off(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
-// byte offset of element column `m` (16-bit) of image row `k` in a 16-bit MN-major image (256-B rows)
+// byte offset of 16-B chunk `c` of image row `row` in a K-major image (KB-byte rows); the XOR
+// makes the 16-row fragment reads (ds_read_b128) conflict-free.
+template <int KB>
+__device__ __forceinline__ int kmaj_off(int row, int c) {
+  if constexpr (KB == 128) return row * 128 + ((c ^ ((row >> 1) & 7)) << 4);
+  else return row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
+}
+// byte offset of element column `m` (16-bit) of image row `k` in a 16-bit MN-major image
+// (256-B rows, 32-B pairs swizzled by t(k): conflict-free ds_read_b64_tr_b16)
 __device__ __forceinline__ int mnmaj16_off(int k, int m) {
   const int c = m >> 3;
   const int t = (k & 3) | (((k >> 3) & 1) << 2);
@@ -134,16 +143,17 @@ __device__ __forceinline__ int mnmaj16_off(int k, int m) {
   return k * 256 + (cp << 4) + ((m & 7) << 1);
 }
 
-template <typename T, bool KMAJ>
-__device__ __forceinline__ void stage_store(char* img, const uint4 (&r)[4]) {
+template <typename T, bool KMAJ, int KB>
+__device__ __forceinline__ void stage_store(char* img, const uint4 (&r)[KB / 32]) {
   constexpr int V = Vec<T>::n;
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < KB / 32; ++i) {
     const int id = tid + GT * i;
     int off;
     if constexpr (KMAJ) {
-      off = kmaj_off(id >> 3, id & 7);
+      constexpr int CPRK = KB / 16;
+      off = kmaj_off<KB>(id / CPRK, id % CPRK);
     } else if constexpr (sizeof(T) == 2) {
       constexpr int CPR = BMT * 2 / 16;
       off = mnmaj16_off(id / CPR, (id % CPR) * V);
@@ -159,26 +169,31 @@ __device__ __forceinline__ void stage_store(char* img, const uint4 (&r)[4]) {
 // VGPR round trip).  The LDS destination of a wave-instruction is linear (base + 16*lane), so the
 // bank swizzles of kmaj_off / mnmaj16_off are applied to the per-lane GLOBAL source address
 // (rule 21 of the CDNA guide).  Rows past the matrix edge are clamped to a valid row: their
-// products only reach discarded outputs.  4 instructions per wave per operand.
-template <typename T, bool KMAJ>
+// products only reach discarded outputs.  KB/32 instructions per wave per operand.
+template <typename T, bool KMAJ, int KB>
 __device__ __forceinline__ void glds_tile(char* img, const T* base, int64_t ld, int rows_lim,
                                           int r0, int kloc) {
   constexpr int V = Vec<T>::n;
+  constexpr int NI = KB / 32;
+  constexpr int BKE = KB / (int)sizeof(T);
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NI; ++i) {
     const T* src;
     char* dst;
-    if constexpr (KMAJ) {                      // image [128 rows][128 B]
-      const int row0 = 32 * w + 8 * i;
-      const int row = row0 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
+    if constexpr (KMAJ) {                      // image [128 rows][KB]
+      constexpr int RPI = 1024 / KB;           // rows per instruction
+      constexpr int CPRK = KB / 16;
+      const int row0 = 32 * w + RPI * i;
+      const int row = row0 + lane / CPRK;
+      const int cp = lane % CPRK;
+      const int c = (KB == 128) ? (cp ^ ((row >> 1) & 7)) : (cp ^ ((row >> 2) & 3));
       const int gr = min(r0 + row, rows_lim - 1);
       src = base + (int64_t)gr * ld + kloc + c * V;
-      dst = img + row0 * 128;
-    } else if constexpr (sizeof(T) == 2) {     // image [64 k][256 B], 32-B pairs swizzled by t(k)
-      const int k0 = 16 * w + 4 * i;
+      dst = img + row0 * KB;
+    } else if constexpr (sizeof(T) == 2) {     // image [BKE k][256 B]
+      const int k0 = (BKE / 4) * w + 4 * i;
       const int k = k0 + (lane >> 4);
       const int cp = lane & 15;
       const int t = (k & 3) | (((k >> 3) & 1) << 2);
@@ -187,8 +202,8 @@ __device__ __forceinline__ void glds_tile(char* img, const T* base, int64_t ld, 
       if (gm >= rows_lim) gm = ((rows_lim - 1) / V) * V;
       src = base + (int64_t)(kloc + k) * ld + gm;
       dst = img + k0 * 256;
-    } else {                                   // f32 image [32 k][512 B]
-      const int k0 = 8 * w + 2 * i;
+    } else {                                   // f32 image [BKE k][512 B]
+      const int k0 = (BKE / 4) * w + 2 * i;
       const int k = k0 + (lane >> 5);
       int gm = r0 + (lane & 31) * V;
       if (gm >= rows_lim) gm = ((rows_lim - 1) / V) * V;
@@ -213,7 +228,7 @@ __device__ __forceinline__ H tr_read(const char* p) {
 }
 
 // 16-bit A/B fragment of one 16-row subtile for k-step ks (32 wide) of the current K-tile.
-template <typename T, bool KMAJ>
+template <typename T, bool KMAJ, int KB>
 __device__ __forceinline__ typename Frag16<T>::t read_frag16(const char* img, int rbase, int ks) {
   typedef typename Frag16<T>::t F;
   typedef typename Frag16<T>::h Hf;
@@ -221,7 +236,7 @@ __device__ __forceinline__ typename Frag16<T>::t read_frag16(const char* img, in
   if constexpr (KMAJ) {
     const int row = rbase + (lane & 15);
     const int c = ks * 4 + (lane >> 4);
-    return *(const F*)(img + kmaj_off(row, c));
+    return *(const F*)(img + kmaj_off<KB>(row, c));
   } else {
     const int i = lane & 15;
     const int k0 = ks * 32 + (lane >> 4) * 8 + (i >> 2);
@@ -236,13 +251,13 @@ __device__ __forceinline__ typename Frag16<T>::t read_frag16(const char* img, in
 }
 
 // f32 fragment: element s (0..3) is the operand value at k = seg*16 + 4*(lane>>4) + s.
-template <bool KMAJ>
+template <bool KMAJ, int KB>
 __device__ __forceinline__ f32x4 read_frag32(const char* img, int rbase, int seg) {
   const int lane = threadIdx.x & 63;
   if constexpr (KMAJ) {
     const int row = rbase + (lane & 15);
     const int c = seg * 4 + (lane >> 4);
-    return *(const f32x4*)(img + kmaj_off(row, c));
+    return *(const f32x4*)(img + kmaj_off<KB>(row, c));
   } else {
     const float* f = (const float*)img;
     const int m = rbase + (lane & 15);
@@ -292,18 +307,18 @@ __device__ __forceinline__ void c_addr(const GemmParams& p, int b0, int b1, void
 }
 
 // ------------------------------------------------------------------ main kernel
-template <typename T, bool AK, bool BK>
+template <typename T, bool AK, bool BK, int KB>
 __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB, int wm, int wn,
                                              f32x4 (&acc)[4][4]) {
   if constexpr (sizeof(T) == 2) {
     typedef typename Frag16<T>::t F;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KB / 64; ++ks) {
       F fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = read_frag16<T, AK>(imgA, wm * 64 + i * 16, ks);
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag16<T, AK, KB>(imgA, wm * 64 + i * 16, ks);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = read_frag16<T, BK>(imgB, wn * 64 + j * 16, ks);
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag16<T, BK, KB>(imgB, wn * 64 + j * 16, ks);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -311,12 +326,12 @@ __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB,
     }
   } else {
 #pragma unroll
-    for (int seg = 0; seg < 2; ++seg) {
+    for (int seg = 0; seg < KB / 64; ++seg) {
       f32x4 fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = read_frag32<AK>(imgA, wm * 64 + i * 16, seg);
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag32<AK, KB>(imgA, wm * 64 + i * 16, seg);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = read_frag32<BK>(imgB, wn * 64 + j * 16, seg);
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag32<BK, KB>(imgB, wn * 64 + j * 16, seg);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -326,6 +341,16 @@ __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB,
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0,
                                                              0);
     }
+  }
+}
+
+__device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in {0,4,8,12,16}
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
   }
 }
 
@@ -402,12 +427,14 @@ __device__ __forceinline__ void store_chunk(const Epi& e, O* cp, int64_t cbase, 
   }
 }
 
-template <typename T, typename O, bool AK, bool BK>
+// KB: bytes per operand row of one K-tile (128 | 64); S: LDS stages (2: prefetch 1 tile, two
+// barriers per tile; >= 3: prefetch S-1 tiles, one barrier per tile).
+template <typename T, typename O, bool AK, bool BK, int KB, int S>
 __global__ __launch_bounds__(GT, 2) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TILE_BYTES = 16384;     // one operand image per stage
-  constexpr bool F32 = sizeof(T) == 4;
-  constexpr int BKE = F32 ? 32 : 64;    // K elements per tile
+  constexpr int TILE_BYTES = BMT * KB;  // one operand image per stage
+  constexpr int BKE = KB / (int)sizeof(T);   // K elements per tile
+  constexpr int VMT = 2 * (KB / 32);         // glds instructions per wave per tile
 
   // XCD-aware remap (bijective): consecutive logical tiles (same A row panel) on one XCD.
   const int nwg = p.tiles_m * p.tiles_n;
@@ -446,38 +473,53 @@ __global__ __launch_bounds__(GT, 2) void gemm_kernel(GemmParams p) {
     const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, b0, b1, p.a_kseg, k0, ka);
     const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, b0, b1, p.b_kseg, k0, kb);
     char* base = smem + buf * 2 * TILE_BYTES;
-    glds_tile<T, AK>(base, A, p.lda, p.M, m0, ka);
-    glds_tile<T, BK>(base + TILE_BYTES, B, p.ldb, p.N, n0, kb);
+    glds_tile<T, AK, KB>(base, A, p.lda, p.M, m0, ka);
+    glds_tile<T, BK, KB>(base + TILE_BYTES, B, p.ldb, p.N, n0, kb);
   };
 
-  if (nfull > 0) issue(0, 0);
-  for (int kt = 0; kt < nfull; ++kt) {
-    if (kt + 1 < nfull) {
-      issue(kt + 1, (kt + 1) & 1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // tile kt landed (8 newer in flight)
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (S == 2) {
+    if (nfull > 0) issue(0, 0);
+    for (int kt = 0; kt < nfull; ++kt) {
+      if (kt + 1 < nfull) {
+        issue(kt + 1, (kt + 1) & 1);
+        wait_vm(VMT);                          // tile kt landed (one newer tile in flight)
+      } else {
+        wait_vm(0);
+      }
+      __builtin_amdgcn_s_barrier();            // ... for every wave of the block
+      const char* imgA = smem + (kt & 1) * 2 * TILE_BYTES;
+      if (!(p.dbg & 1)) compute_tile<T, AK, BK, KB>(imgA, imgA + TILE_BYTES, wm, wn, acc);
+      __builtin_amdgcn_s_barrier();            // buffer (kt&1) free for tile kt+2
     }
-    __builtin_amdgcn_s_barrier();                        // ... for every wave of the block
-    const char* imgA = smem + (kt & 1) * 2 * TILE_BYTES;
-    if (!(p.dbg & 1)) compute_tile<T, AK, BK>(imgA, imgA + TILE_BYTES, wm, wn, acc);
-    __builtin_amdgcn_s_barrier();                        // buffer (kt&1) free for tile kt+2
+  } else {
+    constexpr int D = S - 1;                   // prefetch distance
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+      if (i < nfull) issue(i, i);
+    for (int kt = 0; kt < nfull; ++kt) {
+      const int after = min(D - 1, nfull - 1 - kt);   // tiles issued after kt, in flight
+      wait_vm(after * VMT);
+      __builtin_amdgcn_s_barrier();            // tile kt landed for all waves; tile kt-1 consumed
+      if (kt + D < nfull) issue(kt + D, (kt + D) % S);
+      const char* imgA = smem + (kt % S) * 2 * TILE_BYTES;
+      if (!(p.dbg & 1)) compute_tile<T, AK, BK, KB>(imgA, imgA + TILE_BYTES, wm, wn, acc);
+    }
   }
   if (tail) {   // trailing partial K-tile: masked register staging
-    uint4 ra[4], rb[4];
+    uint4 ra[KB / 32], rb[KB / 32];
     const int k0 = kbeg + nfull * BKE;
     int ka, kb;
     const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, b0, b1, p.a_kseg, k0, ka);
     const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, b0, b1, p.b_kseg, k0, kb);
     const int ka_lim = (p.a_mode == 2) ? min(p.a_kseg, ka + (kend - k0)) : kend;
     const int kb_lim = (p.b_mode == 2) ? min(p.b_kseg, kb + (kend - k0)) : kend;
-    stage_load<T, AK>(ra, A, p.lda, p.M, m0, ka_lim, ka);
-    stage_load<T, BK>(rb, B, p.ldb, p.N, n0, kb_lim, kb);
-    char* base = smem + (nfull & 1) * 2 * TILE_BYTES;
-    stage_store<T, AK>(base, ra);
-    stage_store<T, BK>(base + TILE_BYTES, rb);
+    stage_load<T, AK, KB>(ra, A, p.lda, p.M, m0, ka_lim, ka);
+    stage_load<T, BK, KB>(rb, B, p.ldb, p.N, n0, kb_lim, kb);
+    char* base = smem + (nfull % S) * 2 * TILE_BYTES;
+    stage_store<T, AK, KB>(base, ra);
+    stage_store<T, BK, KB>(base + TILE_BYTES, rb);
     __syncthreads();
-    if (!(p.dbg & 1)) compute_tile<T, AK, BK>(base, base + TILE_BYTES, wm, wn, acc);
+    if (!(p.dbg & 1)) compute_tile<T, AK, BK, KB>(base, base + TILE_BYTES, wm, wn, acc);
   }
   __syncthreads();
 
@@ -633,19 +675,42 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   }
 }
 
+template <typename T, typename O, bool AK, bool BK, int KB, int S>
+static void launch_cfg(const GemmParams& p, dim3 grid, hipStream_t st) {
+  constexpr size_t lds = (size_t)S * 2 * BMT * KB;
+  auto fn = gemm_kernel<T, O, AK, BK, KB, S>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(fn, grid, dim3(GT), lds, st, p);
+}
+
+// GEMM configurations: (KB, S) = 1: (128, 2)  2: (128, 3)  3: (64, 3)  4: (64, 4)
+template <typename T, typename O, bool AK, bool BK>
+static void launch_layout(const GemmParams& p, int cfg, dim3 grid, hipStream_t st) {
+  switch (cfg) {
+    case 2: launch_cfg<T, O, AK, BK, 128, 3>(p, grid, st); break;
+    case 3: launch_cfg<T, O, AK, BK, 64, 3>(p, grid, st); break;
+    case 4: launch_cfg<T, O, AK, BK, 64, 4>(p, grid, st); break;
+    default: launch_cfg<T, O, AK, BK, 128, 2>(p, grid, st); break;
+  }
+}
+
 template <typename T, typename O>
-static void launch_to(const GemmParams& p, int ak, int bk, dim3 grid, hipStream_t st) {
-  const size_t lds = 4 * 16384;
-  if (ak && bk) hipLaunchKernelGGL((gemm_kernel<T, O, true, true>), grid, dim3(GT), lds, st, p);
-  else if (ak && !bk) hipLaunchKernelGGL((gemm_kernel<T, O, true, false>), grid, dim3(GT), lds, st, p);
-  else if (!ak && bk) hipLaunchKernelGGL((gemm_kernel<T, O, false, true>), grid, dim3(GT), lds, st, p);
-  else hipLaunchKernelGGL((gemm_kernel<T, O, false, false>), grid, dim3(GT), lds, st, p);
+static void launch_to(const GemmParams& p, int ak, int bk, int cfg, dim3 grid, hipStream_t st) {
+  if (ak && bk) launch_layout<T, O, true, true>(p, cfg, grid, st);
+  else if (ak && !bk) launch_layout<T, O, true, false>(p, cfg, grid, st);
+  else if (!ak && bk) launch_layout<T, O, false, true>(p, cfg, grid, st);
+  else launch_layout<T, O, false, false>(p, cfg, grid, st);
 }
 
 template <typename T>
-static void launch_t(const GemmParams& p, int ak, int bk, dim3 grid, hipStream_t st) {
-  if (p.splits > 1 || p.c_dtype == JMT_F32) launch_to<T, float>(p, ak, bk, grid, st);
-  else launch_to<T, T>(p, ak, bk, grid, st);
+static void launch_t(const GemmParams& p, int ak, int bk, int cfg, dim3 grid, hipStream_t st) {
+  if (p.splits > 1 || p.c_dtype == JMT_F32) launch_to<T, float>(p, ak, bk, cfg, grid, st);
+  else launch_to<T, T>(p, ak, bk, cfg, grid, st);
 }
 
 }  // namespace jmt
@@ -653,7 +718,8 @@ static void launch_t(const GemmParams& p, int ak, int bk, dim3 grid, hipStream_t
 using namespace jmt;
 
 static int g_gemm_dbg = 0;
-extern "C" void jmt_gemm_set_debug(int flags) { g_gemm_dbg = flags; }
+static int g_gemm_cfg = 0;
+extern "C" void jmt_gemm_set_debug(int flags) { g_gemm_dbg = flags & 0xff; g_gemm_cfg = flags >> 8; }
 
 extern "C" size_t jmt_gemm_workspace_bytes(int M, int N, int batch, int splits) {
   if (splits <= 1) return 0;
@@ -674,7 +740,10 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   JMT_CHECK_ARG(batch0 * batch1 <= 65535, "jmt_gemm: batch too large");
   const int es = dtype_size(dt);
   const int V = 16 / es;
-  const int BKE = dt == JMT_F32 ? 32 : 64;
+  // pipeline configuration (see launch_layout); K tiles must divide the K-concat segments
+  int cfg = g_gemm_cfg ? g_gemm_cfg : 1;
+  const int KBsel = (cfg == 3 || cfg == 4) ? 64 : 128;
+  const int BKE = KBsel / es;
   JMT_CHECK_ARG(d->n_a >= 1 && d->n_a <= MAXP && d->n_b >= 1 && d->n_b <= MAXP &&
                     d->n_c >= 1 && d->n_c <= MAXP, "jmt_gemm: pointer table size");
   JMT_CHECK_ARG(d->lda % V == 0 && d->ldb % V == 0, "jmt_gemm: lda/ldb must be multiples of %d", V);
@@ -740,9 +809,9 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   }
   hipStream_t st = as_stream(stream);
   dim3 grid(p.tiles_m * p.tiles_n, batch0 * batch1, splits);
-  if (dt == JMT_F32) launch_t<float>(p, d->a_kmajor, d->b_kmajor, grid, st);
-  else if (dt == JMT_BF16) launch_t<__bf16>(p, d->a_kmajor, d->b_kmajor, grid, st);
-  else launch_t<_Float16>(p, d->a_kmajor, d->b_kmajor, grid, st);
+  if (dt == JMT_F32) launch_t<float>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
+  else if (dt == JMT_BF16) launch_t<__bf16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
+  else launch_t<_Float16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
   JMT_LAUNCH_CHECK("jmt_gemm");
   if (splits > 1) {
     const int64_t total = (int64_t)d->M * d->N * batch0 * batch1;

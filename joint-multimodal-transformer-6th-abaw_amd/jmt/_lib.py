@@ -100,6 +100,9 @@ def load(path: str = LIB_PATH):
         fn.argtypes = args
     if lib.jmt_abi_version() != 1:
         raise JMTError("libjmt_hip.so ABI version mismatch")
+    cfg = int(os.environ.get("JMT_GEMM_CFG", "0"))   # development: force a GEMM pipeline config
+    if cfg:
+        lib.jmt_gemm_set_debug(cfg << 8)
     _lib = lib
     return lib
 

@@ -531,6 +531,20 @@ def multihead_attention(query, key, value, in_w, in_b, out_w, out_b, num_heads):
     return linear(o, out_w, out_b)
 
 
+def multihead_attention_shared_query(query, keys, in_w, in_b, out_w, out_b, num_heads):
+    """[nn.MultiheadAttention(query, k, k) for k in keys] with ONE query projection: the
+    reference applies each cross_attention_* module twice to the same query
+    (mm_multi_transformers.py:142-167), so the q = query W_q^T + b_q GEMM is computed once."""
+    E = in_w.shape[1]
+    q = linear(query, in_w, in_b, 0, E)
+    outs = []
+    for key in keys:
+        kv = linear(key, in_w, in_b, E, 2 * E)
+        o = AttnCoreFn.apply(q, kv, kv, E, num_heads, 0, 0, E)
+        outs.append(linear(o, out_w, out_b))
+    return outs
+
+
 # ------------------------------------------------------------------------- stack / transpose
 class StackSeqFn(Function):
     """torch.stack(xs, dim=2) of seq-first (T, B, E) tensors followed by permute(1,0,2,3),

@@ -9,6 +9,7 @@ import torch
 import torch.nn as nn
 
 from jmt import functional as F
+from jmt import streams
 from jmt.nn import Linear, LayerNorm, MLP, MultiheadAttention
 
 __all__ = ["Attention", "SequentialEncoder", "TransformerEncoderBlock",
@@ -112,16 +113,29 @@ class MultimodalTransformer_w_JR(nn.Module):
         v = visual_features.permute(1, 0, 2)          # free: a strided view (:127-129)
         p = physiological_features.permute(1, 0, 2)
         j = joint_representation.permute(1, 0, 2)
-        v = self.visual_encoder(v)
-        p = self.physiological_encoder(p)
-        j = self.joint_representation_encoder(j)
-        ca_v, ca_p, ca_pv = self.cross_attention_v, self.cross_attention_p, self.cross_attention_pv
-        outs = [ca_v(v, p, p)[0],      # :142-167 (key is value in every call)
-                ca_p(p, v, v)[0],
-                ca_pv(j, v, v)[0],
-                ca_v(v, j, j)[0],
-                ca_pv(j, p, p)[0],
-                ca_p(p, j, j)[0]]
+        dev = visual_features.device
+        # the three encoders are independent: concurrent streams (:132-136)
+        v, p, j = streams.run_parallel([lambda: self.visual_encoder(v),
+                                        lambda: self.physiological_encoder(p),
+                                        lambda: self.joint_representation_encoder(j)], dev)
+
+        # six cross-attentions (:142-167, key is value in every call); each module is applied
+        # to the same query twice, so its query projection is computed once
+        def ca(mod, query, keys):
+            return F.multihead_attention_shared_query(
+                query, keys, mod.in_proj_weight, mod.in_proj_bias, mod.out_proj.weight,
+                mod.out_proj.bias, mod.num_heads)
+
+        r_v, r_p, r_pv = streams.run_parallel(
+            [lambda: ca(self.cross_attention_v, v, (p, j)),
+             lambda: ca(self.cross_attention_p, p, (v, j)),
+             lambda: ca(self.cross_attention_pv, j, (v, p))], dev)
+        outs = [r_v[0],      # CA_v(v, p)
+                r_p[0],      # CA_p(p, v)
+                r_pv[0],     # CA_pv(j, v)
+                r_v[1],      # CA_v(v, j)
+                r_pv[1],     # CA_pv(j, p)
+                r_p[1]]      # CA_p(p, j)
         if self.output_format == "SELF_ATTEN":
             # :169-199 — stack to (6, B*T, 512), encoder over the 6-token sequences, MHA, keep
             # token 5.  Only the last query row of the final attention is computed: it is the

@@ -5,6 +5,7 @@ from __future__ import annotations
 import torch.nn as nn
 
 from jmt import functional as F
+from jmt import streams
 from jmt.nn import Linear
 
 from .mm_multi_transformers import (Attention, SequentialEncoder, TransformerEncoderBlock,
@@ -37,10 +38,13 @@ class MultimodalTransformer_wo_JR(nn.Module):
         self.final_layer = Linear(1024, 512)
 
     def forward(self, visual_features, physiological_features):
-        v = self.visual_encoder(visual_features)
-        p = self.physiological_encoder(physiological_features)
+        dev = visual_features.device
+        v, p = streams.run_parallel([lambda: self.visual_encoder(visual_features),
+                                     lambda: self.physiological_encoder(physiological_features)],
+                                    dev)
         vt, pt = v.permute(1, 0, 2), p.permute(1, 0, 2)
-        ov = self.cross_attention_v(vt, pt, pt)[0].permute(1, 0, 2)
-        op = self.cross_attention_p(pt, vt, vt)[0].permute(1, 0, 2)
+        ov, op = streams.run_parallel([lambda: self.cross_attention_v(vt, pt, pt)[0],
+                                       lambda: self.cross_attention_p(pt, vt, vt)[0]], dev)
+        ov, op = ov.permute(1, 0, 2), op.permute(1, 0, 2)
         assert self.output_format == 'FC', self.output_format
         return F.linear((ov, op), self.final_layer.weight, self.final_layer.bias)

@@ -18,6 +18,9 @@ from jmt._lib import BF16, F32  # noqa: E402
 SHAPES = [
     ("fwd 19200x512x512 NT", 19200, 512, 512, True, True, 1, BF16, 1),
     ("fwd qkv 19200x1536x512 NT", 19200, 1536, 512, True, True, 1, BF16, 1),
+    ("fwd b3 19200x512x512 NT", 19200, 512, 512, True, True, 3, BF16, 1),
+    ("fwd b6 19200x512x512 NT", 19200, 512, 512, True, True, 6, BF16, 1),
+    ("fwd 19200x1024x512 NT", 19200, 1024, 512, True, True, 1, BF16, 1),
     ("fwd out1 19200x1024x3072 NT", 19200, 1024, 3072, True, True, 1, BF16, 1),
     ("dgrad 19200x512x512 NN", 19200, 512, 512, True, False, 1, BF16, 1),
     ("wgrad 512x512x19200 TN", 512, 512, 19200, False, False, 1, F32, None),
@@ -27,9 +30,9 @@ SHAPES = [
 ]
 
 
-def run(reps, dbg):
+def run(reps, dbg, cfg=0):
     lib = _lib.load()
-    lib.jmt_gemm_set_debug(dbg)
+    lib.jmt_gemm_set_debug(dbg | (cfg << 8))
     dev = "cuda"
     out = []
     for name, M, N, K, ak, bk, batch, cdt, splits in SHAPES:
@@ -58,7 +61,7 @@ def run(reps, dbg):
         us = s.elapsed_time(e) / reps * 1e3
         fl = 2.0 * M * N * K * batch
         by = (M * K + N * K) * 2 * batch + M * N * c.element_size() * batch
-        r = {"shape": name, "dbg": dbg, "us": round(us, 2), "tflops": round(fl / us / 1e6, 1),
+        r = {"shape": name, "dbg": dbg, "cfg": cfg, "us": round(us, 2), "tflops": round(fl / us / 1e6, 1),
              "gbs": round(by / us / 1e3, 1)}
         out.append(r)
         print(json.dumps(r), flush=True)
@@ -71,8 +74,10 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--dbg", type=int, nargs="*", default=[0])
     ap.add_argument("--only", default="", help="substring filter on shape names")
+    ap.add_argument("--cfg", type=int, nargs="*", default=[0])
     args = ap.parse_args()
     if args.only:
         SHAPES[:] = [s for s in SHAPES if args.only in s[0]]
-    for d in args.dbg:
-        run(args.reps, d)
+    for c in args.cfg:
+        for d in args.dbg:
+            run(args.reps, d, c)
