@@ -76,7 +76,12 @@ typedef struct jmt_gemm_desc {
 
 int jmt_gemm(const jmt_gemm_desc* desc, void* stream);
 size_t jmt_gemm_workspace_bytes(int M, int N, int batch, int splits);
-/* development only: GEMM ablation flags (1 = skip MFMA, 2 = skip epilogue stores), 0 = off */
+/* split-K factor jmt_gemm's planner picks for this problem (1 = no split).  jmt_gemm chooses the
+ * block tile (128x128 or 256x256) from the same cost model: waves x (tile FLOPs / per-block MFMA
+ * rate + per-block overhead) + the split-K reduce traffic. */
+int jmt_gemm_plan_splits(int ab_dtype, int M, int N, int K, int batch);
+/* development only: low byte = GEMM ablation flags (1 = skip MFMA, 2 = skip epilogue stores),
+ * flags >> 8 = forced tile config (1 128x128, 5 256x256, 6 256x128, 7 128x256), 0 = off */
 void jmt_gemm_set_debug(int flags);
 
 /* ------------------------------------------------------------------ row-wise ops

@@ -6,30 +6,38 @@
 // (NN) and wgrad (TN, split-K over the B*T tokens), and the attention products S = Q K^T,
 // O = P V and their backward (batched over (batch, head) with two batch strides).
 //
-// Design (see DESIGN.md §GEMM):
-//  * 256 threads = 4 waves in a 2x2 grid, block tile 128x128, wave tile 64x64 = 4x4 MFMA tiles.
-//  * 16-bit inputs: v_mfma_f32_16x16x32_{bf16,f16}, BK = 64.  f32 inputs (the fp32 parity mode):
-//    v_mfma_f32_16x16x4_f32 (exact f32 fma chain), BK = 32.  Either way one K-tile is 128 bytes
-//    per row, so the staging code is shared.
-//  * Each operand is staged global -> registers -> LDS (double-buffered, loads of tile k+1 issued
-//    before the MFMAs of tile k, LDS writes after them: T14).  The LDS image depends on the
-//    operand's memory order:
+// Design (DESIGN.md §4):
+//  * Tile configurations (TileCfg): block tile BM x BN computed by WM x WN waves, each wave a
+//    (BM/WM) x (BN/WN) tile of 16x16 MFMA sub-tiles.  16-bit inputs: v_mfma_f32_16x16x32_{bf16,
+//    f16}; f32 inputs (the fp32 parity mode): v_mfma_f32_16x16x4_f32 (exact f32 fma chain).
+//      cfg 1: 128x128, 2x2 waves  (256 threads, 2 blocks / CU)   — small / batched problems
+//      cfg 5: 256x256, 2x4 waves  (512 threads, 1 block / CU)    — large problems: 2x the
+//             FLOPs per byte staged into LDS.  The planner (plan()) picks tile and split-K from
+//             a cost model; 256x128 / 128x256 tiles and 3-5 stage KB=64 pipelines measured slower
+//             on every JMT shape (profiles/r01_gemm_tiles.txt).
+//    A K-tile is KB = 128 bytes per operand row (64 elements of 16-bit, 32 of f32).
+//  * Operands are staged by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction, no
+//    VGPR round trip) into S = 2 LDS stages.  The LDS image depends on the operand's memory order:
 //      K-major operand  -> image [row][k], 16-B chunks XOR-swizzled by (row>>1)&7, read with
 //                          ds_read_b128 (conflict-free for the 16-row fragment reads);
-//      MN-major operand -> image [k][row] copied straight (no register transpose), 32-B pairs
-//                          swizzled by t(k), read with ds_read_b64_tr_b16 (T10) for 16-bit types.
+//      MN-major operand -> image [k][row], 32-B pairs swizzled by t(k), read with
+//                          ds_read_b64_tr_b16 (hardware transpose) for 16-bit types.
+//    The LDS-DMA destination is linear per wave-instruction, so swizzles go on the per-lane
+//    GLOBAL source address.  A trailing partial K-tile is staged through registers with masks.
 //  * Operands may be K-concatenations of up to 8 tensors (cat(...) @ W^T without a concat copy)
 //    or per-batch pointer tables; C may be a per-batch pointer table.
+//  * The MFMA is fed (B, A), so each accumulator holds a TRANSPOSED 16x16 tile: a lane owns one
+//    C row and 4 consecutive columns, and the epilogue stores straight from registers (8-B
+//    bf16 / 16-B fp32 stores, 16 rows x 64 B per instruction) with alpha, bias (per column / per
+//    row), beta*C, ReLU and the ReLU-backward mask fused — no LDS round trip, no barriers
+//    (measured 10-15% faster than an LDS-staged 16-B-row epilogue).
 //  * split-K writes fp32 partial slabs to a caller-owned workspace; jmt_gemm launches the
 //    reduce + epilogue kernel afterwards (deterministic, no atomics).
-//  * XCD-aware block -> tile remap: blocks that share an A row panel run on the same XCD (T1).
+//  * XCD-aware bijective block -> tile remap: blocks sharing an A row panel run on one XCD.
 #include "common.h"
 
 namespace jmt {
 
-constexpr int GT = 256;     // threads per block
-constexpr int BMT = 128;    // block tile rows (M)
-constexpr int BNT = 128;    // block tile cols (N)
 constexpr int MAXP = 8;
 
 struct GemmParams {
@@ -42,7 +50,7 @@ struct GemmParams {
   int64_t lda, ldb, ldc, ldaux;
   int64_t sA0, sA1, sB0, sB1, sC0, sC1;
   int a_mode, b_mode, c_mode;   // 0 strided, 1 pointer per b0, 2 K-concat (a/b only)
-  int a_kseg, b_kseg;           // K-concat segment length (multiple of BK)
+  int a_kseg, b_kseg;           // K-concat segment length (multiple of the K-tile)
   int M, N, K;
   int batch0, batch1;
   int splits, k_per_split;
@@ -52,9 +60,23 @@ struct GemmParams {
   int c_dtype;
   int aux_dtype;
   int tiles_m, tiles_n;
-  int c_vec;                    // C (and aux) rows 16-B aligned for 16-B vector stores
-  int dbg;                      // development ablations: 1 skip MFMA, 2 skip epilogue stores
+  int c_vec4;                   // C (and aux) 4-element groups aligned for 4-element stores
+  int dbg;                      // development ablations: 1 skip MFMA, 2 skip epilogue
 };
+
+template <int BM_, int BN_, int WM_, int WN_, int KB_, int S_>
+struct TileCfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, KB = KB_, S = S_;
+  static constexpr int NT = 64 * WM * WN;          // threads per block
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int TM = WTM / 16, TN = WTN / 16;
+  static constexpr int STAGE = (BM + BN) * KB;     // LDS bytes per stage (A image + B image)
+  static constexpr int EPI = 64 * (BN + 4) * 4;     // epilogue staging of one 64-row pass
+  static constexpr int LDS = S * STAGE > EPI ? S * STAGE : EPI;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+using Cfg1 = TileCfg<128, 128, 2, 2, 128, 2>;
+using Cfg5 = TileCfg<256, 256, 2, 4, 128, 2>;
 
 template <typename T> struct Vec { static constexpr int n = 16 / sizeof(T); };
 
@@ -73,30 +95,81 @@ __device__ __forceinline__ const T* operand_base(const void* const* ptrs, int mo
   return p + (mode == 1 ? 0 : (int64_t)b0 * s0) + (int64_t)b1 * s1;
 }
 
-// K-tile geometry: KB = bytes per operand row of one K-tile (128 or 64), BKE = KB / sizeof(T)
-// K elements.  Register staging (used only for a trailing partial K-tile): each thread moves
-// KB/32 chunks of 16 B per operand.  K-major image: 128 rows x KB/16 chunks; MN-major image:
-// BKE rows x (128*sizeof(T)/16) chunks.
-template <typename T, bool KMAJ, int KB>
-__device__ __forceinline__ void stage_load(uint4 (&r)[KB / 32], const T* base, int64_t ld,
-                                           int rows_lim, int r0, int k_lim, int kloc) {
+// Swizzles.  K-major image: ROWS rows of KB bytes; MN-major image: KB/sizeof(T) k-rows of
+// RB = ROWS*sizeof(T) bytes.
+template <int KB>
+__device__ __forceinline__ int swz_k(int row) {
+  if constexpr (KB == 128) return (row >> 1) & 7;
+  else return (row >> 2) & 3;
+}
+__device__ __forceinline__ int swz_t(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+// Physical 16-B chunk `id` (image byte id*16) -> its logical source element (row index in the
+// M/N dimension, k index) of one K-tile.  Shared by the LDS-DMA and the register paths, whose LDS
+// writes are therefore both linear.
+template <typename T, bool KMAJ, int KB, int ROWS>
+__device__ __forceinline__ void chunk_src(int id, int& row, int& kk) {
   constexpr int V = Vec<T>::n;
-  const int tid = threadIdx.x;
+  if constexpr (KMAJ) {
+    constexpr int CPR = KB / 16;
+    row = id / CPR;
+    const int cp = id % CPR;
+    kk = (cp ^ swz_k<KB>(row)) * V;
+  } else {
+    constexpr int CPR = ROWS * (int)sizeof(T) / 16;
+    kk = id / CPR;
+    const int cp = id % CPR;
+    const int c = (sizeof(T) == 2) ? ((((cp >> 1) ^ swz_t(kk)) << 1) | (cp & 1)) : cp;
+    row = c * V;
+  }
+}
+
+// LDS-DMA staging of one FULL K-tile of one operand (ROWS*KB bytes = ROWS*KB/1024 wave
+// instructions spread over the block's waves).  Rows past the matrix edge are clamped to a valid
+// row: their products only reach discarded outputs.
+template <typename T, bool KMAJ, int KB, int ROWS, int NT>
+__device__ __forceinline__ void glds_tile(char* img, const T* base, int64_t ld, int rows_lim,
+                                          int r0, int kloc) {
+  constexpr int V = Vec<T>::n;
+  constexpr int NW = NT / 64;
+  constexpr int NI = ROWS * KB / 1024 / NW;
+  static_assert(NI >= 1, "tile too small for the block");
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
 #pragma unroll
-  for (int i = 0; i < KB / 32; ++i) {
-    const int id = tid + GT * i;
+  for (int i = 0; i < NI; ++i) {
+    const int q = w * NI + i;               // wave-instruction index = 1 KiB of the image
     int row, kk;
+    chunk_src<T, KMAJ, KB, ROWS>(q * 64 + lane, row, kk);
+    const T* src;
     if constexpr (KMAJ) {
-      constexpr int CPRK = KB / 16;
-      row = id / CPRK;
-      kk = (id % CPRK) * V;
+      const int gr = min(r0 + row, rows_lim - 1);
+      src = base + (int64_t)gr * ld + kloc + kk;
     } else {
-      constexpr int CPR = BMT * (int)sizeof(T) / 16;   // chunks per image row
-      kk = id / CPR;
-      row = (id % CPR) * V;
+      int gm = r0 + row;
+      if (gm >= rows_lim) gm = ((rows_lim - 1) / V) * V;
+      src = base + (int64_t)(kloc + kk) * ld + gm;
     }
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(img + q * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// Register staging of one (partial, masked) K-tile: NC chunks of 16 B per thread.
+template <typename T, bool KMAJ, int KB, int ROWS, int NT>
+__device__ __forceinline__ void stage_tile(char* img, const T* base, int64_t ld, int rows_lim,
+                                           int r0, int k_lim, int kloc) {
+  constexpr int V = Vec<T>::n;
+  constexpr int NC = ROWS * KB / 16 / NT;
+  uint4 r[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int id = threadIdx.x + NT * i;
+    int row, kk;
+    chunk_src<T, KMAJ, KB, ROWS>(id, row, kk);
     const int gr = r0 + row;
-    const int gk = kloc + kk;   // k index local to the operand segment
+    const int gk = kloc + kk;
     uint4 v = make_uint4(0, 0, 0, 0);
     if constexpr (KMAJ) {
       if (gr < rows_lim && gk < k_lim) {
@@ -125,94 +198,8 @@ __device__ __forceinline__ void stage_load(uint4 (&r)[KB / 32], const T* base, i
     }
     r[i] = v;
   }
-}
-
-// byte offset of 16-B chunk `c` of image row `row` in a K-major image (KB-byte rows); the XOR
-// makes the 16-row fragment reads (ds_read_b128) conflict-free.
-template <int KB>
-__device__ __forceinline__ int kmaj_off(int row, int c) {
-  if constexpr (KB == 128) return row * 128 + ((c ^ ((row >> 1) & 7)) << 4);
-  else return row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
-}
-// byte offset of element column `m` (16-bit) of image row `k` in a 16-bit MN-major image
-// (256-B rows, 32-B pairs swizzled by t(k): conflict-free ds_read_b64_tr_b16)
-__device__ __forceinline__ int mnmaj16_off(int k, int m) {
-  const int c = m >> 3;
-  const int t = (k & 3) | (((k >> 3) & 1) << 2);
-  const int cp = ((((c >> 1) ^ t)) << 1) | (c & 1);
-  return k * 256 + (cp << 4) + ((m & 7) << 1);
-}
-
-template <typename T, bool KMAJ, int KB>
-__device__ __forceinline__ void stage_store(char* img, const uint4 (&r)[KB / 32]) {
-  constexpr int V = Vec<T>::n;
-  const int tid = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < KB / 32; ++i) {
-    const int id = tid + GT * i;
-    int off;
-    if constexpr (KMAJ) {
-      constexpr int CPRK = KB / 16;
-      off = kmaj_off<KB>(id / CPRK, id % CPRK);
-    } else if constexpr (sizeof(T) == 2) {
-      constexpr int CPR = BMT * 2 / 16;
-      off = mnmaj16_off(id / CPR, (id % CPR) * V);
-    } else {
-      constexpr int CPR = BMT * 4 / 16;
-      off = (id / CPR) * (BMT * 4) + (id % CPR) * 16;
-    }
-    *(uint4*)(img + off) = r[i];
-  }
-}
-
-// LDS-DMA staging of one FULL K-tile (global_load_lds_dwordx4, 1 KiB per wave-instruction, no
-// VGPR round trip).  The LDS destination of a wave-instruction is linear (base + 16*lane), so the
-// bank swizzles of kmaj_off / mnmaj16_off are applied to the per-lane GLOBAL source address
-// (rule 21 of the CDNA guide).  Rows past the matrix edge are clamped to a valid row: their
-// products only reach discarded outputs.  KB/32 instructions per wave per operand.
-template <typename T, bool KMAJ, int KB>
-__device__ __forceinline__ void glds_tile(char* img, const T* base, int64_t ld, int rows_lim,
-                                          int r0, int kloc) {
-  constexpr int V = Vec<T>::n;
-  constexpr int NI = KB / 32;
-  constexpr int BKE = KB / (int)sizeof(T);
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const T* src;
-    char* dst;
-    if constexpr (KMAJ) {                      // image [128 rows][KB]
-      constexpr int RPI = 1024 / KB;           // rows per instruction
-      constexpr int CPRK = KB / 16;
-      const int row0 = 32 * w + RPI * i;
-      const int row = row0 + lane / CPRK;
-      const int cp = lane % CPRK;
-      const int c = (KB == 128) ? (cp ^ ((row >> 1) & 7)) : (cp ^ ((row >> 2) & 3));
-      const int gr = min(r0 + row, rows_lim - 1);
-      src = base + (int64_t)gr * ld + kloc + c * V;
-      dst = img + row0 * KB;
-    } else if constexpr (sizeof(T) == 2) {     // image [BKE k][256 B]
-      const int k0 = (BKE / 4) * w + 4 * i;
-      const int k = k0 + (lane >> 4);
-      const int cp = lane & 15;
-      const int t = (k & 3) | (((k >> 3) & 1) << 2);
-      const int c = ((((cp >> 1) ^ t)) << 1) | (cp & 1);
-      int gm = r0 + c * V;
-      if (gm >= rows_lim) gm = ((rows_lim - 1) / V) * V;
-      src = base + (int64_t)(kloc + k) * ld + gm;
-      dst = img + k0 * 256;
-    } else {                                   // f32 image [BKE k][512 B]
-      const int k0 = (BKE / 4) * w + 2 * i;
-      const int k = k0 + (lane >> 5);
-      int gm = r0 + (lane & 31) * V;
-      if (gm >= rows_lim) gm = ((rows_lim - 1) / V) * V;
-      src = base + (int64_t)(kloc + k) * ld + gm;
-      dst = img + k0 * 512;
-    }
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-  }
+  for (int i = 0; i < NC; ++i) *(uint4*)(img + (threadIdx.x + NT * i) * 16) = r[i];
 }
 
 // ------------------------------------------------------------------ fragment reads
@@ -227,8 +214,20 @@ __device__ __forceinline__ H tr_read(const char* p) {
   return __builtin_bit_cast(H, v);
 }
 
-// 16-bit A/B fragment of one 16-row subtile for k-step ks (32 wide) of the current K-tile.
-template <typename T, bool KMAJ, int KB>
+template <int KB>
+__device__ __forceinline__ int kmaj_off(int row, int c) {
+  return row * KB + ((c ^ swz_k<KB>(row)) << 4);
+}
+template <int RB>
+__device__ __forceinline__ int mnmaj16_off(int k, int m) {
+  const int c = m >> 3;
+  const int cp = ((((c >> 1) ^ swz_t(k))) << 1) | (c & 1);
+  return k * RB + (cp << 4) + ((m & 7) << 1);
+}
+
+// 16-bit A/B fragment of one 16-row sub-tile for k-step ks (32 wide) of the current K-tile:
+// lane l holds X[row rbase + (l&15)][k = 32 ks + 8 (l>>4) + j], j = 0..7.
+template <typename T, bool KMAJ, int KB, int ROWS>
 __device__ __forceinline__ typename Frag16<T>::t read_frag16(const char* img, int rbase, int ks) {
   typedef typename Frag16<T>::t F;
   typedef typename Frag16<T>::h Hf;
@@ -238,11 +237,12 @@ __device__ __forceinline__ typename Frag16<T>::t read_frag16(const char* img, in
     const int c = ks * 4 + (lane >> 4);
     return *(const F*)(img + kmaj_off<KB>(row, c));
   } else {
+    constexpr int RB = ROWS * 2;
     const int i = lane & 15;
     const int k0 = ks * 32 + (lane >> 4) * 8 + (i >> 2);
     const int m = rbase + (i & 3) * 4;
-    Hf lo = tr_read<Hf>(img + mnmaj16_off(k0, m));
-    Hf hi = tr_read<Hf>(img + mnmaj16_off(k0 + 4, m));
+    Hf lo = tr_read<Hf>(img + mnmaj16_off<RB>(k0, m));
+    Hf hi = tr_read<Hf>(img + mnmaj16_off<RB>(k0 + 4, m));
     F f;
     f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
     f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
@@ -251,7 +251,7 @@ __device__ __forceinline__ typename Frag16<T>::t read_frag16(const char* img, in
 }
 
 // f32 fragment: element s (0..3) is the operand value at k = seg*16 + 4*(lane>>4) + s.
-template <bool KMAJ, int KB>
+template <bool KMAJ, int KB, int ROWS>
 __device__ __forceinline__ f32x4 read_frag32(const char* img, int rbase, int seg) {
   const int lane = threadIdx.x & 63;
   if constexpr (KMAJ) {
@@ -263,10 +263,10 @@ __device__ __forceinline__ f32x4 read_frag32(const char* img, int rbase, int seg
     const int m = rbase + (lane & 15);
     const int k = seg * 16 + 4 * (lane >> 4);
     f32x4 r;
-    r[0] = f[(k + 0) * BMT + m];
-    r[1] = f[(k + 1) * BMT + m];
-    r[2] = f[(k + 2) * BMT + m];
-    r[3] = f[(k + 3) * BMT + m];
+    r[0] = f[(k + 0) * ROWS + m];
+    r[1] = f[(k + 1) * ROWS + m];
+    r[2] = f[(k + 2) * ROWS + m];
+    r[3] = f[(k + 3) * ROWS + m];
     return r;
   }
 }
@@ -278,163 +278,80 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-// ------------------------------------------------------------------ epilogue
-__device__ __forceinline__ float epi_value(const GemmParams& p, float v, int m, int n,
-                                           const void* cptr, int64_t coff, const void* auxp,
-                                           int64_t auxoff) {
-  v *= p.alpha;
-  if (p.bias_mode == 1) v += p.bias[n];
-  else if (p.bias_mode == 2) v += p.bias[m];
-  if (p.beta != 0.f) v += p.beta * ld_dyn(cptr, coff, p.c_dtype);
-  if (p.relu) v = fmaxf(v, 0.f);
-  if (auxp) {
-    if (!(ld_dyn(auxp, auxoff, p.aux_dtype) > 0.f)) v = 0.f;
-  }
-  return v;
-}
-
-__device__ __forceinline__ void c_addr(const GemmParams& p, int b0, int b1, void*& cp,
-                                       int64_t& cbase, const void*& ap, int64_t& abase) {
-  if (p.c_mode == 1) {
-    cp = p.c_ptr[b0];
-    cbase = (int64_t)b1 * p.sC1;
-  } else {
-    cp = p.c_ptr[0];
-    cbase = (int64_t)b0 * p.sC0 + (int64_t)b1 * p.sC1;
-  }
-  ap = p.aux;
-  abase = cbase;   // aux shares C's batch strides (only used unbatched)
-}
-
-// ------------------------------------------------------------------ main kernel
-template <typename T, bool AK, bool BK, int KB>
+template <typename T, bool AK, bool BK, class C>
 __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB, int wm, int wn,
-                                             f32x4 (&acc)[4][4]) {
+                                             f32x4 (&acc)[C::TM][C::TN]) {
   if constexpr (sizeof(T) == 2) {
     typedef typename Frag16<T>::t F;
 #pragma unroll
-    for (int ks = 0; ks < KB / 64; ++ks) {
-      F fa[4], fb[4];
+    for (int ks = 0; ks < C::KB / 64; ++ks) {
+      F fb[C::TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = read_frag16<T, AK, KB>(imgA, wm * 64 + i * 16, ks);
+      for (int j = 0; j < C::TN; ++j)
+        fb[j] = read_frag16<T, BK, C::KB, C::BN>(imgB, wn * C::WTN + j * 16, ks);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = read_frag16<T, BK, KB>(imgB, wn * 64 + j * 16, ks);
+      for (int i = 0; i < C::TM; ++i) {
+        const F fa = read_frag16<T, AK, C::KB, C::BM>(imgA, wm * C::WTM + i * 16, ks);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
+        for (int j = 0; j < C::TN; ++j) acc[i][j] = mfma16(fb[j], fa, acc[i][j]);   // C^T tile
+      }
     }
   } else {
 #pragma unroll
-    for (int seg = 0; seg < KB / 64; ++seg) {
-      f32x4 fa[4], fb[4];
+    for (int seg = 0; seg < C::KB / 64; ++seg) {
+      f32x4 fb[C::TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = read_frag32<AK, KB>(imgA, wm * 64 + i * 16, seg);
+      for (int j = 0; j < C::TN; ++j)
+        fb[j] = read_frag32<BK, C::KB, C::BN>(imgB, wn * C::WTN + j * 16, seg);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = read_frag32<BK, KB>(imgB, wn * 64 + j * 16, seg);
+      for (int i = 0; i < C::TM; ++i) {
+        const f32x4 fa = read_frag32<AK, C::KB, C::BM>(imgA, wm * C::WTM + i * 16, seg);
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0,
-                                                             0);
+          for (int j = 0; j < C::TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[j][s], fa[s], acc[i][j], 0, 0, 0);
+      }
     }
   }
 }
 
-__device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in {0,4,8,12,16}
+__device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n) for small constants
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
   }
 }
 
-template <typename O> struct OutVec { static constexpr int n = 16 / sizeof(O); };
-
-struct Epi {
-  float alpha, beta;
-  const float* bias;
-  int bias_mode, relu, N;
-  int64_t ldc, ldaux;
-};
-
-// Epilogue of one output row chunk of VO = 16/sizeof(O) columns at (m, n); v[] = fp32
-// accumulators.  16-B vector accesses when the chunk is interior and aligned (vec).
-template <typename O>
-__device__ __forceinline__ void store_chunk(const Epi& e, O* cp, int64_t cbase, const O* aux,
-                                            int m, int n, float (&v)[16 / sizeof(O)], bool vec) {
-  constexpr int VO = 16 / sizeof(O);
-  const int64_t co = cbase + (int64_t)m * e.ldc + n;
-  const bool full = vec && (n + VO <= e.N);
-  const int nv = min(VO, e.N - n);
-  float add[VO];
-#pragma unroll
-  for (int i = 0; i < VO; ++i) add[i] = 0.f;
-  if (e.bias_mode == 1) {
-#pragma unroll
-    for (int i = 0; i < VO; ++i) add[i] = (i < nv) ? e.bias[n + i] : 0.f;
-  } else if (e.bias_mode == 2) {
-    const float bm = e.bias[m];
-#pragma unroll
-    for (int i = 0; i < VO; ++i) add[i] = bm;
-  }
-  if (e.beta != 0.f) {
-    O old[VO];
-    if (full) {
-      *(uint4*)old = *(const uint4*)(cp + co);
-    } else {
-#pragma unroll
-      for (int i = 0; i < VO; ++i) old[i] = (i < nv) ? cp[co + i] : from_f<O>(0.f);
-    }
-#pragma unroll
-    for (int i = 0; i < VO; ++i) add[i] += e.beta * to_f(old[i]);
-  }
-  O out[VO];
-  if (aux) {
-    const int64_t ao = cbase + (int64_t)m * e.ldaux + n;
-    O av[VO];
-    if (full) {
-      *(uint4*)av = *(const uint4*)(aux + ao);
-    } else {
-#pragma unroll
-      for (int i = 0; i < VO; ++i) av[i] = (i < nv) ? aux[ao + i] : from_f<O>(0.f);
-    }
-#pragma unroll
-    for (int i = 0; i < VO; ++i) {
-      float x = v[i] * e.alpha + add[i];
-      if (e.relu) x = fmaxf(x, 0.f);
-      out[i] = from_f<O>(to_f(av[i]) > 0.f ? x : 0.f);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < VO; ++i) {
-      float x = v[i] * e.alpha + add[i];
-      if (e.relu) x = fmaxf(x, 0.f);
-      out[i] = from_f<O>(x);
-    }
-  }
-  if (full) {
-    *(uint4*)(cp + co) = *(const uint4*)out;
-  } else {
-#pragma unroll
-    for (int i = 0; i < VO; ++i)
-      if (i < nv) cp[co + i] = out[i];
+// s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[15:14])
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+// wait until at most n (runtime, < 4) K-tiles of VMT DMA instructions each are outstanding
+template <int VMT>
+__device__ __forceinline__ void wait_tiles(int n) {
+  switch (n) {
+    case 0: wait_vmcnt<0>(); break;
+    case 1: wait_vmcnt<VMT>(); break;
+    case 2: wait_vmcnt<2 * VMT>(); break;
+    default: wait_vmcnt<3 * VMT>(); break;
   }
 }
 
-// KB: bytes per operand row of one K-tile (128 | 64); S: LDS stages (2: prefetch 1 tile, two
-// barriers per tile; >= 3: prefetch S-1 tiles, one barrier per tile).
-template <typename T, typename O, bool AK, bool BK, int KB, int S>
-__global__ __launch_bounds__(GT, 2) void gemm_kernel(GemmParams p) {
+// ------------------------------------------------------------------ main kernel
+template <typename T, typename O, bool AK, bool BK, class C>
+__global__ __launch_bounds__(C::NT, 2 * 256 / C::NT > 0 ? 2 * 256 / C::NT : 1)
+void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TILE_BYTES = BMT * KB;  // one operand image per stage
-  constexpr int BKE = KB / (int)sizeof(T);   // K elements per tile
-  constexpr int VMT = 2 * (KB / 32);         // glds instructions per wave per tile
+  constexpr int BKE = C::KB / (int)sizeof(T);         // K elements per tile
+  constexpr int IA = C::BM * C::KB;                   // A image bytes
+  constexpr int VMT = (C::BM + C::BN) * C::KB / 1024 / (C::NT / 64);   // DMA instr / wave / tile
 
   // XCD-aware remap (bijective): consecutive logical tiles (same A row panel) on one XCD.
   const int nwg = p.tiles_m * p.tiles_n;
@@ -450,7 +367,7 @@ __global__ __launch_bounds__(GT, 2) void gemm_kernel(GemmParams p) {
   const int b0 = b / p.batch1, b1 = b % p.batch1;
   const int split = blockIdx.z;
 
-  const int m0 = tm * BMT, n0 = tn * BNT;
+  const int m0 = tm * C::BM, n0 = tn * C::BN;
   const int kbeg = split * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int klen = max(0, kend - kbeg);
@@ -459,25 +376,26 @@ __global__ __launch_bounds__(GT, 2) void gemm_kernel(GemmParams p) {
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / C::WN, wn = wid % C::WN;
 
-  f32x4 acc[4][4];
+  f32x4 acc[C::TM][C::TN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto issue = [&](int kt, int buf) {
     const int k0 = kbeg + kt * BKE;
     int ka, kb;
     const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, b0, b1, p.a_kseg, k0, ka);
     const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, b0, b1, p.b_kseg, k0, kb);
-    char* base = smem + buf * 2 * TILE_BYTES;
-    glds_tile<T, AK, KB>(base, A, p.lda, p.M, m0, ka);
-    glds_tile<T, BK, KB>(base + TILE_BYTES, B, p.ldb, p.N, n0, kb);
+    char* base = smem + buf * C::STAGE;
+    glds_tile<T, AK, C::KB, C::BM, C::NT>(base, A, p.lda, p.M, m0, ka);
+    glds_tile<T, BK, C::KB, C::BN, C::NT>(base + IA, B, p.ldb, p.N, n0, kb);
   };
 
-  if constexpr (S == 2) {
+  if constexpr (C::S == 2) {
+    // prefetch one tile, two barriers per tile
     if (nfull > 0) issue(0, 0);
     for (int kt = 0; kt < nfull; ++kt) {
       if (kt + 1 < nfull) {
@@ -487,56 +405,54 @@ __global__ __launch_bounds__(GT, 2) void gemm_kernel(GemmParams p) {
         wait_vm(0);
       }
       __builtin_amdgcn_s_barrier();            // ... for every wave of the block
-      const char* imgA = smem + (kt & 1) * 2 * TILE_BYTES;
-      if (!(p.dbg & 1)) compute_tile<T, AK, BK, KB>(imgA, imgA + TILE_BYTES, wm, wn, acc);
+      const char* img = smem + (kt & 1) * C::STAGE;
+      if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
       __builtin_amdgcn_s_barrier();            // buffer (kt&1) free for tile kt+2
     }
   } else {
-    constexpr int D = S - 1;                   // prefetch distance
+    // S-1 tiles in flight, one barrier per tile: the barrier of iteration kt also certifies that
+    // every wave finished computing tile kt-1, whose buffer receives tile kt+S-1.
+    static_assert(C::S <= 5, "wait_tiles covers up to 3 newer tiles");
 #pragma unroll
-    for (int i = 0; i < D; ++i)
+    for (int i = 0; i < C::S - 1; ++i)
       if (i < nfull) issue(i, i);
     for (int kt = 0; kt < nfull; ++kt) {
-      const int after = min(D - 1, nfull - 1 - kt);   // tiles issued after kt, in flight
-      wait_vm(after * VMT);
-      __builtin_amdgcn_s_barrier();            // tile kt landed for all waves; tile kt-1 consumed
-      if (kt + D < nfull) issue(kt + D, (kt + D) % S);
-      const char* imgA = smem + (kt % S) * 2 * TILE_BYTES;
-      if (!(p.dbg & 1)) compute_tile<T, AK, BK, KB>(imgA, imgA + TILE_BYTES, wm, wn, acc);
+      wait_tiles<VMT>(min(C::S - 2, nfull - 1 - kt));
+      __builtin_amdgcn_s_barrier();
+      if (kt + C::S - 1 < nfull) issue(kt + C::S - 1, (kt + C::S - 1) % C::S);
+      const char* img = smem + (kt % C::S) * C::STAGE;
+      if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
     }
   }
   if (tail) {   // trailing partial K-tile: masked register staging
-    uint4 ra[KB / 32], rb[KB / 32];
     const int k0 = kbeg + nfull * BKE;
     int ka, kb;
     const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, b0, b1, p.a_kseg, k0, ka);
     const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, b0, b1, p.b_kseg, k0, kb);
     const int ka_lim = (p.a_mode == 2) ? min(p.a_kseg, ka + (kend - k0)) : kend;
     const int kb_lim = (p.b_mode == 2) ? min(p.b_kseg, kb + (kend - k0)) : kend;
-    stage_load<T, AK, KB>(ra, A, p.lda, p.M, m0, ka_lim, ka);
-    stage_load<T, BK, KB>(rb, B, p.ldb, p.N, n0, kb_lim, kb);
-    char* base = smem + (nfull % S) * 2 * TILE_BYTES;
-    stage_store<T, AK, KB>(base, ra);
-    stage_store<T, BK, KB>(base + TILE_BYTES, rb);
+    char* base = smem + (nfull % C::S) * C::STAGE;
+    stage_tile<T, AK, C::KB, C::BM, C::NT>(base, A, p.lda, p.M, m0, ka_lim, ka);
+    stage_tile<T, BK, C::KB, C::BN, C::NT>(base + IA, B, p.ldb, p.N, n0, kb_lim, kb);
     __syncthreads();
-    if (!(p.dbg & 1)) compute_tile<T, AK, BK, KB>(base, base + TILE_BYTES, wm, wn, acc);
+    if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(base, base + IA, wm, wn, acc);
   }
   __syncthreads();
 
-  // ---- epilogue through LDS, one 64-row half at a time: C/D layout of 16x16 MFMA is
-  //      col = lane&15, row = 4*(lane>>4) + r; the store pass writes 16-B row chunks.
-  constexpr int CLD = 132;                  // padded fp32 row of the staged half tile
-  float* ct = (float*)smem;
+  // ---- epilogue.  acc[i][j] holds the TRANSPOSED 16x16 tile (the MFMA was fed B as its first
+  //      operand): lane owns C row (lane&15) and the 4 consecutive columns 4*(lane>>4) + r.
   const bool partial = p.splits > 1;
   O* cp;
   int64_t cbase;
-  const void* ap = partial ? nullptr : p.aux;
-  bool vec;
-  if (partial) {
+  float alpha = p.alpha, beta = p.beta;
+  int bias_mode = p.bias_mode, relu = p.relu;
+  int64_t ldc = p.ldc;
+  const O* auxp = partial ? nullptr : (const O*)p.aux;
+  if (partial) {   // raw partial sums: no epilogue ops, row stride N
     const int nb = p.batch0 * p.batch1;
     cp = (O*)(p.ws + ((int64_t)split * nb + b) * (int64_t)p.M * p.N);
     cbase = 0;
-    vec = (p.N % 4) == 0;
+    alpha = 1.f; beta = 0.f; bias_mode = 0; relu = 0; ldc = p.N;
   } else {
     if (p.c_mode == 1) {
       cp = (O*)p.c_ptr[b0];
@@ -545,157 +461,153 @@ __global__ __launch_bounds__(GT, 2) void gemm_kernel(GemmParams p) {
       cp = (O*)p.c_ptr[0];
       cbase = (int64_t)b0 * p.sC0 + (int64_t)b1 * p.sC1;
     }
-    vec = p.c_vec != 0;
   }
   if (p.dbg & 2) {
     float sum = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      for (int j = 0; j < C::TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
     if (sum == 12345.678f) ((float*)cp)[0] = sum;   // keep acc live
     return;
   }
-  Epi ep;
-  ep.alpha = p.alpha; ep.beta = p.beta; ep.bias = p.bias; ep.bias_mode = p.bias_mode;
-  ep.relu = p.relu; ep.N = p.N; ep.ldc = p.ldc; ep.ldaux = p.ldaux;
-  if (partial) {   // raw partial sums: no epilogue ops, row stride N
-    ep.alpha = 1.f; ep.beta = 0.f; ep.bias_mode = 0; ep.relu = 0; ep.ldc = p.N;
-  }
-  const O* auxp = (const O*)ap;
-  constexpr int VO = OutVec<O>::n;
-  constexpr int CPR = BNT / VO;                 // chunks per 128-col row
-  constexpr int RPI = GT / CPR;                 // rows covered per pass
-  constexpr int NIT = 64 / RPI;                 // passes per 64-row half
-  // each thread owns ONE column chunk for the whole epilogue (GT is a multiple of CPR)
-  const int cc = (threadIdx.x % CPR) * VO;
-  const int r_in = threadIdx.x / CPR;
-  const int n = n0 + cc;
-  const bool col_ok = n < p.N;
-  const int nv = min(VO, p.N - n);
-  const bool full = vec && (n + VO <= p.N);
-  float bvec[VO];
+  {
+    // direct epilogue: 4 consecutive columns per lane -> one 8-B (16-bit) / 16-B (fp32) store,
+    // 16 rows x 4 lanes per instruction; no LDS round trip, no block barriers.
+    const int rl = lane & 15, cq = 4 * (lane >> 4);
+    const bool vec4 = partial ? (p.N % 4) == 0 : p.c_vec4 != 0;
+    float bias4[C::TN][4];
 #pragma unroll
-  for (int i = 0; i < VO; ++i) bvec[i] = 0.f;
-  if (ep.bias_mode == 1 && col_ok) {
+    for (int j = 0; j < C::TN; ++j) {
+      const int n = n0 + wn * C::WTN + 16 * j + cq;
 #pragma unroll
-    for (int i = 0; i < VO; ++i) bvec[i] = (i < nv) ? ep.bias[n + i] : 0.f;
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (wm == h) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            ct[(i * 16 + 4 * (lane >> 4) + r) * CLD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+      for (int e = 0; e < 4; ++e)
+        bias4[j][e] = (bias_mode == 1 && n + e < p.N) ? p.bias[n + e] : 0.f;
     }
-    __syncthreads();
-    // phase 1: LDS reads + every global load of the pass (C_old, aux) issued back to back
-    float v[NIT][VO];
-    O oldv[NIT][VO];
-    O auxv[NIT][VO];
+    const bool plain = beta == 0.f && auxp == nullptr;
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int rr = r_in + RPI * it;
-      const float* src = ct + rr * CLD + cc;
+    for (int i = 0; i < C::TM; ++i) {
+      const int m = m0 + wm * C::WTM + 16 * i + rl;
+      if (m >= p.M) continue;
+      const float bm = (bias_mode == 2) ? p.bias[m] : 0.f;
+      const int64_t rowo = cbase + (int64_t)m * ldc;
+      const int64_t rowa = cbase + (int64_t)m * p.ldaux;
 #pragma unroll
-      for (int e = 0; e < VO; e += 4) {
-        const float4 t = *(const float4*)(src + e);
-        v[it][e] = t.x; v[it][e + 1] = t.y; v[it][e + 2] = t.z; v[it][e + 3] = t.w;
-      }
-      const int m = m0 + 64 * h + rr;
-      const bool ok = col_ok && m < p.M;
-      const int64_t co = cbase + (int64_t)m * ep.ldc + n;
-      const int64_t ao = cbase + (int64_t)m * ep.ldaux + n;
-      if (ep.beta != 0.f) {
-        if (ok && full) *(uint4*)oldv[it] = *(const uint4*)(cp + co);
-        else
+      for (int j = 0; j < C::TN; ++j) {
+        const int n = n0 + wn * C::WTN + 16 * j + cq;
+        if (n >= p.N) continue;
+        const bool full4 = vec4 && n + 4 <= p.N;
+        float x[4];
 #pragma unroll
-          for (int i = 0; i < VO; ++i) oldv[it][i] = (ok && i < nv) ? cp[co + i] : from_f<O>(0.f);
-      }
-      if (auxp) {
-        if (ok && full) *(uint4*)auxv[it] = *(const uint4*)(auxp + ao);
-        else
+        for (int e = 0; e < 4; ++e) x[e] = acc[i][j][e] * alpha + bias4[j][e] + bm;
+        if (!plain) {
 #pragma unroll
-          for (int i = 0; i < VO; ++i) auxv[it][i] = (ok && i < nv) ? auxp[ao + i] : from_f<O>(0.f);
+          for (int e = 0; e < 4; ++e) {
+            if (n + e < p.N) {
+              if (beta != 0.f) x[e] += beta * to_f(cp[rowo + n + e]);
+              if (relu) x[e] = fmaxf(x[e], 0.f);
+              if (auxp && !(to_f(auxp[rowa + n + e]) > 0.f)) x[e] = 0.f;
+            }
+          }
+        } else if (relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = fmaxf(x[e], 0.f);
+        }
+        if (full4) {
+          if constexpr (sizeof(O) == 4) {
+            *(float4*)(cp + rowo + n) = make_float4(x[0], x[1], x[2], x[3]);
+          } else {
+            O o4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o4[e] = from_f<O>(x[e]);
+            *(uint2*)(cp + rowo + n) = *(const uint2*)o4;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < p.N) cp[rowo + n + e] = from_f<O>(x[e]);
+        }
       }
     }
-    // phase 2: epilogue math + 16-B stores
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int rr = r_in + RPI * it;
-      const int m = m0 + 64 * h + rr;
-      if (!(col_ok && m < p.M)) continue;
-      const float bm = (ep.bias_mode == 2) ? ep.bias[m] : 0.f;
-      O out[VO];
-#pragma unroll
-      for (int i = 0; i < VO; ++i) {
-        float x = v[it][i] * ep.alpha + bvec[i] + bm;
-        if (ep.beta != 0.f) x += ep.beta * to_f(oldv[it][i]);
-        if (ep.relu) x = fmaxf(x, 0.f);
-        if (auxp && !(to_f(auxv[it][i]) > 0.f)) x = 0.f;
-        out[i] = from_f<O>(x);
-      }
-      const int64_t co = cbase + (int64_t)m * ep.ldc + n;
-      if (full) {
-        *(uint4*)(cp + co) = *(const uint4*)out;
-      } else {
-#pragma unroll
-        for (int i = 0; i < VO; ++i)
-          if (i < nv) cp[co + i] = out[i];
-      }
-    }
-    __syncthreads();
   }
 }
 
-// split-K reduction + epilogue: one thread per output element (vector of 4 along n when possible)
+// split-K reduction + epilogue.  Vector form (N % 4 == 0, C 4-element aligned): one thread per 4
+// consecutive outputs, float4 slab loads; otherwise one thread per output element.
+template <typename O, bool V4>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
+  constexpr int W = V4 ? 4 : 1;
   const int nb = p.batch0 * p.batch1;
   const int64_t per = (int64_t)p.M * p.N;
-  const int64_t total = per * nb;
+  const int64_t total = per * nb / W;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
-    const int b = (int)(e / per);
-    const int64_t mn = e - (int64_t)b * per;
+    const int64_t idx = e * W;
+    const int b = (int)(idx / per);
+    const int64_t mn = idx - (int64_t)b * per;
     const int m = (int)(mn / p.N), n = (int)(mn - (int64_t)m * p.N);
-    float v = 0.f;
-    for (int s = 0; s < p.splits; ++s) v += p.ws[((int64_t)s * nb + b) * per + mn];
+    float v[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) v[i] = 0.f;
+    for (int s = 0; s < p.splits; ++s) {
+      const float* src = p.ws + ((int64_t)s * nb + b) * per + mn;
+      if constexpr (V4) {
+        const float4 t = *(const float4*)src;
+        v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
+      } else {
+        v[0] += *src;
+      }
+    }
     const int b0 = b / p.batch1, b1 = b % p.batch1;
-    void* cp;
-    int64_t cbase, abase;
-    const void* ap;
-    c_addr(p, b0, b1, cp, cbase, ap, abase);
+    O* cp;
+    int64_t cbase;
+    if (p.c_mode == 1) {
+      cp = (O*)p.c_ptr[b0];
+      cbase = (int64_t)b1 * p.sC1;
+    } else {
+      cp = (O*)p.c_ptr[0];
+      cbase = (int64_t)b0 * p.sC0 + (int64_t)b1 * p.sC1;
+    }
     const int64_t co = cbase + (int64_t)m * p.ldc + n;
-    const int64_t ao = abase + (int64_t)m * p.ldaux + n;
-    st_dyn(cp, co, p.c_dtype, epi_value(p, v, m, n, cp, co, ap, ao));
+    const O* auxp = (const O*)p.aux;
+    O out[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      float x = v[i] * p.alpha;
+      if (p.bias_mode == 1) x += p.bias[n + i];
+      else if (p.bias_mode == 2) x += p.bias[m];
+      if (p.beta != 0.f) x += p.beta * to_f(cp[co + i]);
+      if (p.relu) x = fmaxf(x, 0.f);
+      if (auxp && !(to_f(auxp[cbase + (int64_t)m * p.ldaux + n + i]) > 0.f)) x = 0.f;
+      out[i] = from_f<O>(x);
+    }
+    if constexpr (V4) {
+      if constexpr (sizeof(O) == 4) *(float4*)(cp + co) = *(const float4*)out;
+      else *(uint2*)(cp + co) = *(const uint2*)out;
+    } else {
+      cp[co] = out[0];
+    }
   }
 }
 
-template <typename T, typename O, bool AK, bool BK, int KB, int S>
+// ------------------------------------------------------------------ launch
+template <typename T, typename O, bool AK, bool BK, class C>
 static void launch_cfg(const GemmParams& p, dim3 grid, hipStream_t st) {
-  constexpr size_t lds = (size_t)S * 2 * BMT * KB;
-  auto fn = gemm_kernel<T, O, AK, BK, KB, S>;
+  auto fn = gemm_kernel<T, O, AK, BK, C>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+                              C::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL(fn, grid, dim3(GT), lds, st, p);
+  hipLaunchKernelGGL(fn, grid, dim3(C::NT), (size_t)C::LDS, st, p);
 }
 
-// GEMM configurations: (KB, S) = 1: (128, 2)  2: (128, 3)  3: (64, 3)  4: (64, 4)
 template <typename T, typename O, bool AK, bool BK>
 static void launch_layout(const GemmParams& p, int cfg, dim3 grid, hipStream_t st) {
   switch (cfg) {
-    case 2: launch_cfg<T, O, AK, BK, 128, 3>(p, grid, st); break;
-    case 3: launch_cfg<T, O, AK, BK, 64, 3>(p, grid, st); break;
-    case 4: launch_cfg<T, O, AK, BK, 64, 4>(p, grid, st); break;
-    default: launch_cfg<T, O, AK, BK, 128, 2>(p, grid, st); break;
+    case 5: launch_cfg<T, O, AK, BK, Cfg5>(p, grid, st); break;
+    default: launch_cfg<T, O, AK, BK, Cfg1>(p, grid, st); break;
   }
 }
 
@@ -713,6 +625,62 @@ static void launch_t(const GemmParams& p, int ak, int bk, int cfg, dim3 grid, hi
   else launch_to<T, T>(p, ak, bk, cfg, grid, st);
 }
 
+static void cfg_tile(int cfg, int& bm, int& bn) {
+  switch (cfg) {
+    case 5: bm = 256; bn = 256; break;
+    default: bm = 128; bn = 128; break;
+  }
+}
+
+// ------------------------------------------------------------------ planner
+// Cost model fitted to the gfx950 microbenchmarks (scripts/bench_gemm.py, profiles/r01_*):
+//   t(cfg, splits) = ceil(blocks / resident slots) * (tile FLOPs / per-block rate + overhead)
+//                  + split-K reduce (fp32 slabs read once, output written once) when splits > 1
+// 128x128 runs 2 blocks / CU (512 slots) at ~1.9 TFLOP/s each; 256x256 runs 1 block / CU at
+// ~4.2 TFLOP/s (half the LDS traffic per FLOP) but quantises 4x coarser.  Waves are counted
+// whole: the tail wave of a launch costs a full wave.
+struct TileModel { int id, bm, bn, slots; double mflop_per_us, ovh_us; };
+static const TileModel kModels16[] = {{1, 128, 128, 512, 1.91, 7.0},
+                                      {5, 256, 256, 256, 4.2, 13.0}};
+static const TileModel kModels32[] = {{1, 128, 128, 512, 0.5, 7.0}};
+
+static double model_cost(const TileModel& t, int M, int N, int K, int batch, int splits, int bke) {
+  const long tiles = (long)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn) * batch;
+  int kps = ((K + splits - 1) / splits + bke - 1) / bke * bke;
+  if (kps < bke) kps = bke;
+  const long blocks = tiles * splits;
+  const long waves = (blocks + t.slots - 1) / t.slots;
+  const double tile_mflop = 2.0 * t.bm * t.bn * (double)kps / 1e6;
+  double c = waves * (tile_mflop / t.mflop_per_us + t.ovh_us);
+  if (splits > 1) c += ((double)splits + 1.0) * M * N * batch * 4.0 / 3.5e6 + 4.0;
+  return c;
+}
+
+// Padding guard: the 256x256 tile is only considered when it wastes < 10% of its MACs.
+static bool tile_ok(const TileModel& t, int M, int N) {
+  const double pad = (double)((M + t.bm - 1) / t.bm * t.bm) * ((N + t.bn - 1) / t.bn * t.bn);
+  return t.bm == 128 || (double)M * N >= 0.9 * pad;
+}
+
+static void plan(int dt, int M, int N, int K, int batch, int fixed_splits, int& cfg, int& splits) {
+  const int bke = 128 / dtype_size(dt);
+  const TileModel* ms = dt == JMT_F32 ? kModels32 : kModels16;
+  const int nm = dt == JMT_F32 ? 1 : 2;
+  double best = 1e300;
+  cfg = 1;
+  splits = fixed_splits > 0 ? fixed_splits : 1;
+  for (int i = 0; i < nm; ++i) {
+    if (!tile_ok(ms[i], M, N)) continue;
+    int s_lo = 1, s_hi = 32;
+    if (fixed_splits > 0) s_lo = s_hi = fixed_splits;
+    for (int s = s_lo; s <= s_hi; ++s) {
+      if (fixed_splits <= 0 && s > 1 && K / s < 4 * bke) break;   // >= 4 K-tiles per split
+      const double c = model_cost(ms[i], M, N, K, batch, s, bke);
+      if (c < best * 0.999) { best = c; cfg = ms[i].id; splits = s; }
+    }
+  }
+}
+
 }  // namespace jmt
 
 using namespace jmt;
@@ -720,6 +688,14 @@ using namespace jmt;
 static int g_gemm_dbg = 0;
 static int g_gemm_cfg = 0;
 extern "C" void jmt_gemm_set_debug(int flags) { g_gemm_dbg = flags & 0xff; g_gemm_cfg = flags >> 8; }
+
+extern "C" int jmt_gemm_plan_splits(int ab_dtype, int M, int N, int K, int batch) {
+  if (M <= 0 || N <= 0 || K <= 0) return 1;
+  if (ab_dtype != JMT_F32 && ab_dtype != JMT_BF16 && ab_dtype != JMT_F16) return 1;
+  int cfg, splits;
+  plan(ab_dtype, M, N, K, batch < 1 ? 1 : batch, 0, cfg, splits);
+  return splits;
+}
 
 extern "C" size_t jmt_gemm_workspace_bytes(int M, int N, int batch, int splits) {
   if (splits <= 1) return 0;
@@ -740,10 +716,7 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   JMT_CHECK_ARG(batch0 * batch1 <= 65535, "jmt_gemm: batch too large");
   const int es = dtype_size(dt);
   const int V = 16 / es;
-  // pipeline configuration (see launch_layout); K tiles must divide the K-concat segments
-  int cfg = g_gemm_cfg ? g_gemm_cfg : 1;
-  const int KBsel = (cfg == 3 || cfg == 4) ? 64 : 128;
-  const int BKE = KBsel / es;
+  const int BKE = 128 / es;     // K elements per K-tile (all configs use 128-B tile rows)
   JMT_CHECK_ARG(d->n_a >= 1 && d->n_a <= MAXP && d->n_b >= 1 && d->n_b <= MAXP &&
                     d->n_c >= 1 && d->n_c <= MAXP, "jmt_gemm: pointer table size");
   JMT_CHECK_ARG(d->lda % V == 0 && d->ldb % V == 0, "jmt_gemm: lda/ldb must be multiples of %d", V);
@@ -781,20 +754,17 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   p.relu = d->relu;
   p.c_dtype = d->c_dtype;
   p.aux_dtype = d->aux_dtype;
-  p.tiles_m = (d->M + BMT - 1) / BMT;
-  p.tiles_n = (d->N + BNT - 1) / BNT;
   p.dbg = g_gemm_dbg;
   {
     const int ces = dtype_size(d->c_dtype);
-    const int VO = 16 / ces;
-    bool cv = d->ldc % VO == 0 && d->sC0 % VO == 0 && d->sC1 % VO == 0;
-    for (int i = 0; i < d->n_c; ++i) cv = cv && (((uintptr_t)d->c[i] & 15) == 0);
-    if (d->aux) cv = cv && (((uintptr_t)d->aux & 15) == 0) && d->ldaux % VO == 0;
-    p.c_vec = cv ? 1 : 0;
+    bool cv4 = d->ldc % 4 == 0 && d->sC0 % 4 == 0 && d->sC1 % 4 == 0;
+    for (int i = 0; i < d->n_c; ++i) cv4 = cv4 && (((uintptr_t)d->c[i] & (4 * ces - 1)) == 0);
+    if (d->aux) cv4 = cv4 && (((uintptr_t)d->aux & (4 * ces - 1)) == 0) && d->ldaux % 4 == 0;
+    p.c_vec4 = cv4 ? 1 : 0;
   }
 
   int splits = d->splits < 1 ? 1 : d->splits;
-  // each split must own whole K-tiles, and a K-concat segment boundary must not cut a tile
+  // each split owns whole K-tiles, so a K-concat segment boundary never cuts a tile
   int kps = ((d->K + splits - 1) / splits + BKE - 1) / BKE * BKE;
   if (kps < BKE) kps = BKE;
   splits = (d->K + kps - 1) / kps;
@@ -807,6 +777,15 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
     JMT_CHECK_ARG(d->workspace != nullptr && d->ws_bytes >= need,
                   "jmt_gemm: split-K needs %zu workspace bytes", need);
   }
+  int cfg = g_gemm_cfg;
+  if (!cfg) {
+    int s_unused;
+    plan(dt, d->M, d->N, d->K, batch0 * batch1, splits, cfg, s_unused);
+  }
+  int bm, bn;
+  cfg_tile(cfg, bm, bn);
+  p.tiles_m = (d->M + bm - 1) / bm;
+  p.tiles_n = (d->N + bn - 1) / bn;
   hipStream_t st = as_stream(stream);
   dim3 grid(p.tiles_m * p.tiles_n, batch0 * batch1, splits);
   if (dt == JMT_F32) launch_t<float>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
@@ -814,10 +793,17 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   else launch_t<_Float16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
   JMT_LAUNCH_CHECK("jmt_gemm");
   if (splits > 1) {
-    const int64_t total = (int64_t)d->M * d->N * batch0 * batch1;
+    const bool v4 = d->N % 4 == 0 && p.c_vec4;
+    const int64_t total = (int64_t)d->M * d->N * batch0 * batch1 / (v4 ? 4 : 1);
     int blocks = (int)((total + 255) / 256);
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, p);
+    if (blocks > 8192) blocks = 8192;
+#define JMT_SKR(O)                                                                          \
+    if (v4) hipLaunchKernelGGL((splitk_reduce_kernel<O, true>), dim3(blocks), dim3(256), 0, st, p); \
+    else hipLaunchKernelGGL((splitk_reduce_kernel<O, false>), dim3(blocks), dim3(256), 0, st, p);
+    if (d->c_dtype == JMT_F32) { JMT_SKR(float) }
+    else if (d->c_dtype == JMT_BF16) { JMT_SKR(__bf16) }
+    else { JMT_SKR(_Float16) }
+#undef JMT_SKR
     JMT_LAUNCH_CHECK("jmt_gemm(splitk_reduce)");
   }
   return JMT_OK;

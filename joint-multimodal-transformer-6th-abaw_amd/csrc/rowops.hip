@@ -267,29 +267,98 @@ __global__ __launch_bounds__(RB) void ln_bwd_kernel(int64_t rows, int D, const T
   }
 }
 
-// sum partial slabs: out[c] (+)= sum_b partials[b*stride + off + c]
-// block = 64 columns x 4 slab groups; slabs strided over the groups, reduced through LDS.
-__global__ __launch_bounds__(RB) void slab_reduce_kernel(int nblk, int D, const float* partials,
-                                                         int64_t stride, int64_t off, float* out,
-                                                         int beta_acc) {
+// sum partial slabs: for c < W, v = sum_b partials[b*stride + c];  c < split -> out0[c],
+// else out1[c - split]  ((+)= with beta_acc).  Block = 4 column quads (16 columns) x 64 slab
+// groups: each thread streams ~nblk/64 float4 loads with 4 independent accumulators, then a
+// fixed-order two-level LDS reduction (deterministic).  W % 4 == 0, stride % 4 == 0.
+constexpr int SR_G = 64;
+__global__ __launch_bounds__(RB) void slab_reduce_kernel(int nblk, int W, const float* partials,
+                                                         int64_t stride, int split, float* out0,
+                                                         float* out1, int beta_acc) {
+  __shared__ float4 red[SR_G][4];
+  __shared__ float4 red2[16][4];
+  const int q = threadIdx.x & 3, g = threadIdx.x >> 2;
+  const int c = blockIdx.x * 16 + 4 * q;
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
+  if (c < W) {
+    const float* base = partials + c;
+    int b = g;
+    for (; b + 3 * SR_G < nblk; b += 4 * SR_G) {
+      const float4 v0 = *(const float4*)(base + (int64_t)b * stride);
+      const float4 v1 = *(const float4*)(base + (int64_t)(b + SR_G) * stride);
+      const float4 v2 = *(const float4*)(base + (int64_t)(b + 2 * SR_G) * stride);
+      const float4 v3 = *(const float4*)(base + (int64_t)(b + 3 * SR_G) * stride);
+      a0.x += v0.x; a0.y += v0.y; a0.z += v0.z; a0.w += v0.w;
+      a1.x += v1.x; a1.y += v1.y; a1.z += v1.z; a1.w += v1.w;
+      a2.x += v2.x; a2.y += v2.y; a2.z += v2.z; a2.w += v2.w;
+      a3.x += v3.x; a3.y += v3.y; a3.z += v3.z; a3.w += v3.w;
+    }
+    for (; b < nblk; b += SR_G) {
+      const float4 v0 = *(const float4*)(base + (int64_t)b * stride);
+      a0.x += v0.x; a0.y += v0.y; a0.z += v0.z; a0.w += v0.w;
+    }
+  }
+  red[g][q] = make_float4(a0.x + a1.x + a2.x + a3.x, a0.y + a1.y + a2.y + a3.y,
+                          a0.z + a1.z + a2.z + a3.z, a0.w + a1.w + a2.w + a3.w);
+  __syncthreads();
+  if (threadIdx.x < 64) {   // 16 partial groups x 4 quads: each sums 4 of the 64 slab groups
+    const int qq = threadIdx.x & 3, gg = threadIdx.x >> 2;
+    float4 t = red[4 * gg][qq];
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      const float4 u = red[4 * gg + i][qq];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    red2[gg][qq] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4 && blockIdx.x * 16 + 4 * threadIdx.x < W) {
+    float4 t = red2[0][threadIdx.x];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) {
+      const float4 u = red2[i][threadIdx.x];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    const int cc = blockIdx.x * 16 + 4 * threadIdx.x;
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int col = cc + e;
+      float* o = col < split ? out0 + col : out1 + (col - split);
+      *o = beta_acc ? *o + tv[e] : tv[e];
+    }
+  }
+}
+
+// scalar fallback (W or stride not a multiple of 4)
+__global__ __launch_bounds__(RB) void slab_reduce_scalar_kernel(int nblk, int W,
+                                                                const float* partials,
+                                                                int64_t stride, int split,
+                                                                float* out0, float* out1,
+                                                                int beta_acc) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  float s0 = 0.f, s1 = 0.f;
-  if (c < D) {
-    int b = g;
-    for (; b + 4 < nblk; b += 8) {
-      s0 += partials[(int64_t)b * stride + off + c];
-      s1 += partials[(int64_t)(b + 4) * stride + off + c];
-    }
-    for (; b < nblk; b += 4) s0 += partials[(int64_t)b * stride + off + c];
-  }
-  red[g][lane] = s0 + s1;
+  float s0 = 0.f;
+  if (c < W)
+    for (int b = g; b < nblk; b += 4) s0 += partials[(int64_t)b * stride + c];
+  red[g][lane] = s0;
   __syncthreads();
-  if (g == 0 && c < D) {
-    const float s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    out[c] = beta_acc ? out[c] + s : s;
+  if (g == 0 && c < W) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    float* o = c < split ? out0 + c : out1 + (c - split);
+    *o = beta_acc ? *o + t : t;
   }
+}
+
+static void launch_slab_reduce(int nblk, int W, const float* partials, int64_t stride, int split,
+                               float* out0, float* out1, int beta_acc, hipStream_t st) {
+  if (W % 4 == 0 && stride % 4 == 0 && ((uintptr_t)partials & 15) == 0)
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((W + 15) / 16), dim3(RB), 0, st, nblk, W,
+                       partials, stride, split, out0, out1, beta_acc);
+  else
+    hipLaunchKernelGGL(slab_reduce_scalar_kernel, dim3((W + 63) / 64), dim3(RB), 0, st, nblk, W,
+                       partials, stride, split, out0, out1, beta_acc);
 }
 
 // ------------------------------------------------------------------ softmax
@@ -334,34 +403,40 @@ __global__ __launch_bounds__(RB) void softmax_bwd_kernel(int64_t rows, int n, co
 // ------------------------------------------------------------------ column sums (bias grad)
 constexpr int CS_ROWS = 256;
 
-// N % 4 == 0: block = 64 columns (16 quads) x 16 row lanes over CS_ROWS rows
+// 16-B aligned rows: block = 8 column chunks of VE = 16/sizeof(T) elements (8*VE columns) x 32
+// row lanes over CS_ROWS rows; each thread issues CS_ROWS/32 independent 16-B loads.
 template <typename T>
 __global__ __launch_bounds__(RB) void colsum_vec_kernel(int64_t rows, int N, const T* dy,
                                                         int64_t ld, float* partials) {
-  __shared__ float red[16][64];
-  const int q = threadIdx.x & 15, rl = threadIdx.x >> 4;
-  const int c = blockIdx.y * 64 + 4 * q;
+  constexpr int VE = 16 / sizeof(T);
+  constexpr int NC = 8 * VE;                // columns per block
+  __shared__ float red[32][NC + 1];
+  const int q = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c = blockIdx.y * NC + q * VE;
   const int64_t r0 = (int64_t)blockIdx.x * CS_ROWS;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (c < N) {
-#pragma unroll 4
-    for (int i = rl; i < CS_ROWS; i += 16) {
-      const int64_t r = r0 + i;
-      if (r >= rows) break;
-      float v[4];
-      V4<T>::ld(dy + r * ld + c, v);
+  float acc[VE];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[e] += v[e];
+  for (int e = 0; e < VE; ++e) acc[e] = 0.f;
+  if (c < N) {
+#pragma unroll
+    for (int i = 0; i < CS_ROWS / 32; ++i) {
+      const int64_t r = r0 + rl + 32 * i;
+      if (r < rows) {
+        const uint4 u = *(const uint4*)(dy + r * ld + c);
+        const T* v = (const T*)&u;
+#pragma unroll
+        for (int e = 0; e < VE; ++e) acc[e] += to_f(v[e]);
+      }
     }
   }
 #pragma unroll
-  for (int e = 0; e < 4; ++e) red[rl][4 * q + e] = acc[e];
+  for (int e = 0; e < VE; ++e) red[rl][q * VE + e] = acc[e];
   __syncthreads();
-  if (threadIdx.x < 64) {
-    const int cc = blockIdx.y * 64 + threadIdx.x;
+  if (threadIdx.x < NC) {
+    const int cc = blockIdx.y * NC + threadIdx.x;
     float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s += red[i][threadIdx.x];
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) s += red[i][threadIdx.x];
     if (cc < N) partials[(int64_t)blockIdx.x * N + cc] = s;
   }
 }
@@ -483,11 +558,7 @@ extern "C" int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, 
       })));
 #undef JMT_LNB_VEC
   JMT_LAUNCH_CHECK("jmt_layernorm_bwd");
-  const unsigned g = (unsigned)((D + 63) / 64);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(g), dim3(RB), 0, st, nblk, D, partials,
-                     (int64_t)2 * D, (int64_t)0, dgamma, beta_acc);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(g), dim3(RB), 0, st, nblk, D, partials,
-                     (int64_t)2 * D, (int64_t)D, dbeta, beta_acc);
+  launch_slab_reduce(nblk, 2 * D, partials, (int64_t)2 * D, D, dgamma, dbeta, beta_acc, st);
   JMT_LAUNCH_CHECK("jmt_layernorm_bwd(reduce)");
   return JMT_OK;
 }
@@ -528,16 +599,16 @@ extern "C" int jmt_colsum(int dt, int64_t rows, int N, const void* dy, int64_t l
     if (!beta_acc) (void)hipMemsetAsync(db, 0, sizeof(float) * N, st);
     return JMT_OK;
   }
-  const bool vec = (N % 4 == 0) && (ld % 4 == 0) && ((uintptr_t)dy % 8 == 0);
+  const int ve = 16 / dtype_size(dt);
+  const bool vec = (N % ve == 0) && (ld % ve == 0) && ((uintptr_t)dy % 16 == 0);
   JMT_DISPATCH1(dt, T,
       if (vec)
-        hipLaunchKernelGGL((colsum_vec_kernel<T>), dim3(nblk, (N + 63) / 64), dim3(RB), 0, st,
-                           rows, N, (const T*)dy, ld, partials);
+        hipLaunchKernelGGL((colsum_vec_kernel<T>), dim3(nblk, (N + 8 * ve - 1) / (8 * ve)),
+                           dim3(RB), 0, st, rows, N, (const T*)dy, ld, partials);
       else
         hipLaunchKernelGGL((colsum_kernel<T>), dim3(nblk, (N + RB - 1) / RB), dim3(RB), 0, st,
                            rows, N, (const T*)dy, ld, partials));
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((N + 63) / 64), dim3(RB), 0, st, nblk, N,
-                     partials, (int64_t)N, (int64_t)0, db, beta_acc);
+  launch_slab_reduce(nblk, N, partials, (int64_t)N, N, db, db, beta_acc, st);
   JMT_LAUNCH_CHECK("jmt_colsum");
   return JMT_OK;
 }

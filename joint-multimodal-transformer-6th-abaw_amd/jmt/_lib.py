@@ -48,6 +48,7 @@ _PROTOS = {
     "jmt_kernel_count": (c_int, []),
     "jmt_gemm": (c_int, [C.POINTER(GemmDesc), c_vp]),
     "jmt_gemm_workspace_bytes": (C.c_size_t, [c_int, c_int, c_int, c_int]),
+    "jmt_gemm_plan_splits": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "jmt_gemm_set_debug": (None, [c_int]),
     "jmt_l2norm_fwd": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_f,
                                c_vp]),

@@ -47,15 +47,9 @@ def set_launch_hook(hook) -> None:
     _launch_hook = hook
 
 
-def auto_splits(M: int, N: int, K: int, batch: int, bk: int = 64) -> int:
-    """Split-K factor: aim at >= 512 blocks (2 per CU) while keeping >= 8 K-tiles per split."""
-    tiles = math.ceil(M / 128) * math.ceil(N / 128) * batch
-    if tiles >= 512:
-        return 1
-    max_by_k = K // (8 * bk)
-    if max_by_k < 2:
-        return 1
-    return max(1, min(math.ceil(512 / tiles), max_by_k, 32))
+def auto_splits(M: int, N: int, K: int, batch: int, ab_dtype: int) -> int:
+    """Split-K factor from the library's GEMM planner (jmt_gemm_plan_splits)."""
+    return int(_lib.load().jmt_gemm_plan_splits(ab_dtype, M, N, K, batch))
 
 
 def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
@@ -92,7 +86,7 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
     d.relu = int(relu)
     d.aux = aux.data_ptr() if aux is not None else None
     if splits is None:
-        splits = auto_splits(M, N, K, batch0 * batch1, 32 if ab_dtype == F32 else 64)
+        splits = auto_splits(M, N, K, batch0 * batch1, ab_dtype)
     d.splits = splits
     ws = None
     if splits > 1:

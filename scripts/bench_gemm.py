@@ -23,6 +23,8 @@ SHAPES = [
     ("fwd 19200x1024x512 NT", 19200, 1024, 512, True, True, 1, BF16, 1),
     ("fwd out1 19200x1024x3072 NT", 19200, 1024, 3072, True, True, 1, BF16, 1),
     ("dgrad 19200x512x512 NN", 19200, 512, 512, True, False, 1, BF16, 1),
+    ("dgrad out1 19200x3072x1024 NN", 19200, 3072, 1024, True, False, 1, BF16, 1),
+    ("wgrad out1 1024x3072x19200 TN", 1024, 3072, 19200, False, False, 1, F32, None),
     ("wgrad 512x512x19200 TN", 512, 512, 19200, False, False, 1, F32, None),
     ("attn S 300x300x512 b64 NT", 300, 300, 512, True, True, 64, F32, 1),
     ("attn PV 300x512x300 b64 NN", 300, 512, 300, True, False, 64, BF16, 1),
@@ -75,7 +77,25 @@ if __name__ == "__main__":
     ap.add_argument("--dbg", type=int, nargs="*", default=[0])
     ap.add_argument("--only", default="", help="substring filter on shape names")
     ap.add_argument("--cfg", type=int, nargs="*", default=[0])
+    ap.add_argument("--copy", action="store_true", help="also time torch copy/fill of C-sized buffers")
     args = ap.parse_args()
+    if args.copy:
+        for mb in (19.6, 39.3, 78.6):
+            n = int(mb * 1e6 / 2)
+            x = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+            y = torch.empty_like(x)
+            for name, fn, by in (("fill", lambda: y.fill_(1.0), n * 2), ("copy", lambda: y.copy_(x), n * 4)):
+                for _ in range(3):
+                    fn()
+                torch.cuda.synchronize()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(50):
+                    fn()
+                e.record()
+                torch.cuda.synchronize()
+                us = s.elapsed_time(e) / 50 * 1e3
+                print(json.dumps({"op": name, "MB": mb, "us": round(us, 2), "gbs": round(by / us / 1e3, 1)}))
     if args.only:
         SHAPES[:] = [s for s in SHAPES if args.only in s[0]]
     for c in args.cfg:
