@@ -121,6 +121,31 @@ int jmt_softmax_bwd(int p_dt, int ds_dt, int64_t rows, int n, const void* p, int
                     const float* dp, int64_t lddp, float scale, void* ds, int64_t ldds,
                     void* stream);
 
+/* Fused attention core (F.multi_head_attention_forward's softmax(Q K^T * scale) V per (n, h);
+ * mm_multi_transformers.py:57,142-167,191, intra_modal_transformer_fusion.py):
+ * element (l, n, h, d) of X in {q,k,v,o,go,dq} at X + l*sX_l + n*sX_n + h*dh + d.
+ * jmt_attn_supported(dt, dh) != 0 for the configurations the fused kernels cover (16-bit,
+ * dh = 512); otherwise the entry points return JMT_ERR_UNSUPPORTED and the caller uses the
+ * GEMM + jmt_softmax path.
+ * jmt_attn_fwd: writes o and, if lse != NULL, lse[(n*H + h)*Lq + l] = ln sum_k exp(scale s_lk).
+ *   Training: p_out != NULL receives the UNNORMALISED probabilities (N*H*Lq rows of ldp, columns
+ *   [Lk, ldp) zero) and mt (jmt_attn_mt_floats floats) each key tile's reference max;
+ *   jmt_attn_bwd_dq normalises them in place.
+ * jmt_attn_bwd_dq: given dO (go), o, k, v, lse and the forward's p / mt: rewrites p as the exact
+ *   probabilities, writes ds = scale * P o (dO V^T - rowsum(dO o O)) (same layout as p) and
+ *   dq = ds K.  dK = ds^T Q and dV = P^T dO are left to jmt_gemm. */
+int jmt_attn_supported(int dt, int dh);
+int jmt_attn_mt_floats(int N, int H, int Lq, int Lk);
+int jmt_attn_fwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* q, int64_t sq_l,
+                 int64_t sq_n, const void* k, int64_t sk_l, int64_t sk_n, const void* v,
+                 int64_t sv_l, int64_t sv_n, void* o, int64_t so_l, int64_t so_n, float scale,
+                 float* lse, void* p_out, int64_t ldp, float* mt, void* stream);
+int jmt_attn_bwd_dq(int dt, int N, int H, int Lq, int Lk, int dh, const void* go, int64_t sgo_l,
+                    int64_t sgo_n, const void* o, int64_t so_l, int64_t so_n, const void* k,
+                    int64_t sk_l, int64_t sk_n, const void* v, int64_t sv_l, int64_t sv_n,
+                    const float* lse, void* p, const float* mt, int64_t ldp, void* ds, void* dq,
+                    int64_t sdq_l, int64_t sdq_n, float scale, void* stream);
+
 /* Bias gradient: db[n] (+)= sum_m dy[m][n] (two-phase, deterministic, fp32 partial slabs of
  * jmt_colsum_blocks(rows) * N floats). */
 int jmt_colsum_blocks(int64_t rows);

@@ -90,4 +90,39 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 inline hipStream_t as_stream(void* s) { return (hipStream_t)s; }
 
+// ------------------------------------------------------------------ MFMA fragments (gfx950)
+// 16-bit operand fragment of v_mfma_f32_16x16x32_{bf16,f16}: lane l holds row (l&15),
+// k = 8*(l>>4) + j, j = 0..7.  C/D: lane l holds row 4*(l>>4) + r, column l&15.
+template <typename T> struct Frag16;
+template <> struct Frag16<__bf16> { typedef bf16x8 t; typedef bf16x4 h; };
+template <> struct Frag16<_Float16> { typedef f16x8 t; typedef f16x4 h; };
+
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+// ds_read_b64_tr_b16: the 16 lanes of a group that address k rows kb..kb+3 (lane i -> row
+// kb + (i>>2), columns 4*(i&3)..+3) receive, per lane, column (i) of those 4 rows.
+template <typename H>
+__device__ __forceinline__ H tr_read(const char* p) {
+  const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, p));
+  return __builtin_bit_cast(H, v);
+}
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[15:14])
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
 }  // namespace jmt

@@ -203,17 +203,6 @@ __device__ __forceinline__ void stage_tile(char* img, const T* base, int64_t ld,
 }
 
 // ------------------------------------------------------------------ fragment reads
-template <typename T> struct Frag16;
-template <> struct Frag16<__bf16> { typedef bf16x8 t; typedef bf16x4 h; };
-template <> struct Frag16<_Float16> { typedef f16x8 t; typedef f16x4 h; };
-
-typedef short i16x4 __attribute__((ext_vector_type(4)));
-template <typename H>
-__device__ __forceinline__ H tr_read(const char* p) {
-  const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, p));
-  return __builtin_bit_cast(H, v);
-}
-
 template <int KB>
 __device__ __forceinline__ int kmaj_off(int row, int c) {
   return row * KB + ((c ^ swz_k<KB>(row)) << 4);
@@ -271,12 +260,6 @@ __device__ __forceinline__ f32x4 read_frag32(const char* img, int rbase, int seg
   }
 }
 
-__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
 
 template <typename T, bool AK, bool BK, class C>
 __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB, int wm, int wn,
@@ -327,12 +310,6 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n) for sma
   }
 }
 
-// s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[15:14])
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
 // wait until at most n (runtime, < 4) K-tiles of VMT DMA instructions each are outstanding
 template <int VMT>
 __device__ __forceinline__ void wait_tiles(int n) {

@@ -63,6 +63,14 @@ _PROTOS = {
     "jmt_softmax_fwd": (c_int, [c_int, c_i64, c_int, c_vp, c_i64, c_f, c_vp, c_i64, c_vp]),
     "jmt_softmax_bwd": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_i64, c_f, c_vp,
                                 c_i64, c_vp]),
+    "jmt_attn_supported": (c_int, [c_int, c_int]),
+    "jmt_attn_mt_floats": (c_int, [c_int, c_int, c_int, c_int]),
+    "jmt_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp,
+                             c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_f, c_vp,
+                             c_vp, c_i64, c_vp, c_vp]),
+    "jmt_attn_bwd_dq": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
+                                c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
+                                c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_f, c_vp]),
     "jmt_colsum_blocks": (c_int, [c_i64]),
     "jmt_colsum": (c_int, [c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_int, c_vp, c_vp]),
     "jmt_copy2d": (c_int, [c_int, c_int, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,

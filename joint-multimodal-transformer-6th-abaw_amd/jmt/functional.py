@@ -422,6 +422,26 @@ class AttnCoreFn(Function):
     Scores are materialised as fp32 (N, H, Lq, ldS), probabilities in the compute dtype."""
 
     @staticmethod
+    def _probs(q_src, k_src, E, H, qcol, kcol, ldS, scale, cd):
+        """P = softmax(scale Q K^T) as (N, H, Lq, ldS) in the compute dtype (score GEMM into fp32
+        + jmt_softmax_fwd)."""
+        Lq, N = q_src.shape[0], q_src.shape[1]
+        Lk = k_src.shape[0]
+        dh = E // H
+        dev = q_src.device
+        bS = (H * Lq * ldS, Lq * ldS)
+        S = torch.empty(N * H * Lq * ldS, dtype=torch.float32, device=dev)
+        ops.gemm(M=Lq, N=Lk, K=dh, ab_dtype=_dc(cd), c_dtype=F32,
+                 a=[_ptr(q_src, qcol)], lda=q_src.stride(0), a_kmajor=True,
+                 sA=(q_src.stride(1), dh),
+                 b=[_ptr(k_src, kcol)], ldb=k_src.stride(0), b_kmajor=True,
+                 sB=(k_src.stride(1), dh),
+                 c=[S.data_ptr()], ldc=ldS, sC=bS, batch0=N, batch1=H, device=dev)
+        P = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
+        ops.softmax_fwd(S, ldS, N * H * Lq, Lk, scale, P, ldS)
+        return P
+
+    @staticmethod
     def forward(ctx, q_src, k_src, v_src, E, H, qcol, kcol, vcol):
         cd = compute_dtype()
         for t in (q_src, k_src, v_src):
@@ -430,38 +450,44 @@ class AttnCoreFn(Function):
         Lk = k_src.shape[0]
         dh = E // H
         dev = q_src.device
-        sq_l, sq_n = q_src.stride(0), q_src.stride(1)
-        sk_l, sk_n = k_src.stride(0), k_src.stride(1)
-        sv_l, sv_n = v_src.stride(0), v_src.stride(1)
         ldS = _round_up(Lk, 8)
         bS = (H * Lq * ldS, Lq * ldS)
-        S = torch.empty(N * H * Lq * ldS, dtype=torch.float32, device=dev)
-        ops.gemm(M=Lq, N=Lk, K=dh, ab_dtype=_dc(cd), c_dtype=F32,
-                 a=[_ptr(q_src, qcol)], lda=sq_l, a_kmajor=True, sA=(sq_n, dh),
-                 b=[_ptr(k_src, kcol)], ldb=sk_l, b_kmajor=True, sB=(sk_n, dh),
-                 c=[S.data_ptr()], ldc=ldS, sC=bS, batch0=N, batch1=H, device=dev)
-        P = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
         scale = 1.0 / math.sqrt(dh)
-        ops.softmax_fwd(S, ldS, N * H * Lq, Lk, scale, P, ldS)
-        del S
         o = Rows(q_src).like(E, cd)
-        ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
-                 a=[P.data_ptr()], lda=ldS, a_kmajor=True, sA=bS,
-                 b=[_ptr(v_src, vcol)], ldb=sv_l, b_kmajor=False, sB=(sv_n, dh),
-                 c=[o.data_ptr()], ldc=o.stride(0), sC=(o.stride(1), dh),
-                 batch0=N, batch1=H, device=dev)
-        ctx.save_for_backward(q_src, k_src, v_src, P)
+        fused = cd != torch.float32 and ops.attn_supported(_dc(cd), dh)
+        if fused:
+            # one kernel: scores stay on chip (attn.hip); the unnormalised probabilities, the
+            # per-tile maxima and the lse are kept for the fused backward
+            lse = torch.empty(N * H * Lq, dtype=torch.float32, device=dev)
+            P = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
+            mt = torch.empty(max(ops.attn_mt_floats(N, H, Lq, Lk), 1), dtype=torch.float32,
+                             device=dev)
+            ops.attn_fwd(_dc(cd), N, H, Lq, Lk, dh,
+                         _ptr(q_src, qcol), (q_src.stride(0), q_src.stride(1)),
+                         _ptr(k_src, kcol), (k_src.stride(0), k_src.stride(1)),
+                         _ptr(v_src, vcol), (v_src.stride(0), v_src.stride(1)),
+                         o.data_ptr(), (o.stride(0), o.stride(1)), scale, lse, P, ldS, mt)
+            ctx.save_for_backward(q_src, k_src, v_src, P, o, lse, mt)
+        else:
+            P = AttnCoreFn._probs(q_src, k_src, E, H, qcol, kcol, ldS, scale, cd)
+            ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                     a=[P.data_ptr()], lda=ldS, a_kmajor=True, sA=bS,
+                     b=[_ptr(v_src, vcol)], ldb=v_src.stride(0), b_kmajor=False,
+                     sB=(v_src.stride(1), dh),
+                     c=[o.data_ptr()], ldc=o.stride(0), sC=(o.stride(1), dh),
+                     batch0=N, batch1=H, device=dev)
+            ctx.save_for_backward(q_src, k_src, v_src, P, None, None, None)
         # which inputs are the same tensor (saved tensors are not guaranteed to unpack to the
         # same Python objects, so the aliasing is recorded here)
         owner = (0, 0 if k_src is q_src else 1,
                  0 if v_src is q_src else (1 if v_src is k_src else 2))
-        ctx.meta = (E, H, qcol, kcol, vcol, ldS, scale, cd, owner)
+        ctx.meta = (E, H, qcol, kcol, vcol, ldS, scale, cd, owner, fused)
         return o
 
     @staticmethod
     def backward(ctx, go):
-        q_src, k_src, v_src, P = ctx.saved_tensors
-        E, H, qcol, kcol, vcol, ldS, scale, cd, owner = ctx.meta
+        q_src, k_src, v_src, P, o, lse, mt = ctx.saved_tensors
+        E, H, qcol, kcol, vcol, ldS, scale, cd, owner, fused = ctx.meta
         Lq, N = q_src.shape[0], q_src.shape[1]
         Lk = k_src.shape[0]
         dh = E // H
@@ -473,15 +499,10 @@ class AttnCoreFn(Function):
         sk_l, sk_n = k_src.stride(0), k_src.stride(1)
         sv_l, sv_n = v_src.stride(0), v_src.stride(1)
         so_l, so_n = go.stride(0), go.stride(1)
+        if fused and go.data_ptr() % 16:
+            go = go.clone(memory_format=torch.contiguous_format)
+            so_l, so_n = go.stride(0), go.stride(1)
         bS = (H * Lq * ldS, Lq * ldS)
-        dP = torch.empty(N * H * Lq * ldS, dtype=torch.float32, device=dev)
-        ops.gemm(M=Lq, N=Lk, K=dh, ab_dtype=_dc(cd), c_dtype=F32,
-                 a=[go.data_ptr()], lda=so_l, a_kmajor=True, sA=(so_n, dh),
-                 b=[_ptr(v_src, vcol)], ldb=sv_l, b_kmajor=True, sB=(sv_n, dh),
-                 c=[dP.data_ptr()], ldc=ldS, sC=bS, batch0=N, batch1=H, device=dev)
-        dS = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
-        ops.softmax_bwd(P, ldS, dP, ldS, N * H * Lq, Lk, scale, dS, ldS)
-        del dP
         # one gradient buffer per distinct source tensor (packed qkv -> one buffer)
         srcs = (q_src, k_src, v_src)
         bufs = [None, None, None]
@@ -489,12 +510,28 @@ class AttnCoreFn(Function):
             if owner[i] == i:
                 bufs[i] = Rows(srcs[i]).like(srcs[i].shape[-1], cd)
         dq, dk, dv = bufs[owner[0]], bufs[owner[1]], bufs[owner[2]]
-        # dQ = dS K
-        ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
-                 a=[dS.data_ptr()], lda=ldS, a_kmajor=True, sA=bS,
-                 b=[_ptr(k_src, kcol)], ldb=sk_l, b_kmajor=False, sB=(sk_n, dh),
-                 c=[_ptr(dq, qcol)], ldc=dq.stride(0), sC=(dq.stride(1), dh), batch0=N,
-                 batch1=H, device=dev)
+        dS = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
+        if fused:
+            # dP, softmax backward and dQ = dS K in one kernel; P normalised in place
+            ops.attn_bwd_dq(_dc(cd), N, H, Lq, Lk, dh, go.data_ptr(), (so_l, so_n),
+                            o.data_ptr(), (o.stride(0), o.stride(1)),
+                            _ptr(k_src, kcol), (sk_l, sk_n), _ptr(v_src, vcol), (sv_l, sv_n),
+                            lse, P, mt, ldS, dS, _ptr(dq, qcol), (dq.stride(0), dq.stride(1)),
+                            scale)
+        else:
+            dP = torch.empty(N * H * Lq * ldS, dtype=torch.float32, device=dev)
+            ops.gemm(M=Lq, N=Lk, K=dh, ab_dtype=_dc(cd), c_dtype=F32,
+                     a=[go.data_ptr()], lda=so_l, a_kmajor=True, sA=(so_n, dh),
+                     b=[_ptr(v_src, vcol)], ldb=sv_l, b_kmajor=True, sB=(sv_n, dh),
+                     c=[dP.data_ptr()], ldc=ldS, sC=bS, batch0=N, batch1=H, device=dev)
+            ops.softmax_bwd(P, ldS, dP, ldS, N * H * Lq, Lk, scale, dS, ldS)
+            del dP
+            # dQ = dS K
+            ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                     a=[dS.data_ptr()], lda=ldS, a_kmajor=True, sA=bS,
+                     b=[_ptr(k_src, kcol)], ldb=sk_l, b_kmajor=False, sB=(sk_n, dh),
+                     c=[_ptr(dq, qcol)], ldc=dq.stride(0), sC=(dq.stride(1), dh), batch0=N,
+                     batch1=H, device=dev)
         # dK = dS^T Q
         ops.gemm(M=Lk, N=dh, K=Lq, ab_dtype=_dc(cd), c_dtype=_dc(cd),
                  a=[dS.data_ptr()], lda=ldS, a_kmajor=False, sA=bS,

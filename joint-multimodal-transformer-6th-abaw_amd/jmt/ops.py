@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -143,6 +144,36 @@ def softmax_fwd(s, lds, rows, n, scale, p, ldp):
 def softmax_bwd(p, ldp, dp, lddp, rows, n, scale, ds, ldds):
     _lib.call("jmt_softmax_bwd", dt(p), dt(ds), rows, n, p.data_ptr(), ldp, dp.data_ptr(), lddp,
               scale, ds.data_ptr(), ldds, stream())
+
+
+_attn_fused = {"on": os.environ.get("JMT_ATTN_FUSED", "1") != "0"}
+
+
+def attn_supported(dtype: int, dh: int) -> bool:
+    return _attn_fused["on"] and bool(_lib.load().jmt_attn_supported(dtype, dh))
+
+
+def attn_mt_floats(N, H, Lq, Lk) -> int:
+    return int(_lib.load().jmt_attn_mt_floats(N, H, Lq, Lk))
+
+
+def attn_fwd(dtype, N, H, Lq, Lk, dh, q_ptr, sq, k_ptr, sk, v_ptr, sv, o_ptr, so, scale, lse,
+             p=None, ldp=0, mt=None):
+    """Fused softmax(scale Q K^T) V; sq/sk/sv/so = (row stride, batch stride) in elements.
+    With p/mt (training) the unnormalised probabilities and per-tile maxima are kept for
+    attn_bwd_dq."""
+    _ptr = lambda t: t.data_ptr() if t is not None else None
+    _lib.call("jmt_attn_fwd", dtype, N, H, Lq, Lk, dh, q_ptr, sq[0], sq[1], k_ptr, sk[0], sk[1],
+              v_ptr, sv[0], sv[1], o_ptr, so[0], so[1], scale, _ptr(lse), _ptr(p), ldp, _ptr(mt),
+              stream())
+
+
+def attn_bwd_dq(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, k_ptr, sk, v_ptr, sv, lse, p,
+                mt, ldp, ds, dq_ptr, sdq, scale):
+    """dS = scale P o (dO V^T - rowsum(dO o O)) and dQ = dS K; p normalised in place."""
+    _lib.call("jmt_attn_bwd_dq", dtype, N, H, Lq, Lk, dh, go_ptr, sgo[0], sgo[1], o_ptr, so[0],
+              so[1], k_ptr, sk[0], sk[1], v_ptr, sv[0], sv[1], lse.data_ptr(), p.data_ptr(),
+              mt.data_ptr(), ldp, ds.data_ptr(), dq_ptr, sdq[0], sdq[1], scale, stream())
 
 
 def colsum(dy, ld, rows, N, db, beta_acc=False):

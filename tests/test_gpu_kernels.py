@@ -309,3 +309,57 @@ def test_sgd_matches_torch_nesterov():
         opt.step()
     assert (p - p_ref.detach()).abs().max().item() < 1e-6
     assert (shadow.float() - p.bfloat16().float()).abs().max().item() == 0
+
+
+@pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("Lq,Lk,N", [(300, 300, 3), (1, 6, 40), (6, 6, 17), (70, 129, 2),
+                                     (64, 64, 1), (129, 1, 2)])
+def test_fused_attention_fwd_vs_fp32(cd, Lq, Lk, N):
+    """jmt_attn_fwd (attn.hip) on packed self/cross-attention layouts vs softmax(QK^T/sqrt(d))V
+    in fp32 from the same rounded inputs; the log-sum-exp against torch.logsumexp."""
+    E = H_DIM = 512
+    if not ops.attn_supported(ops.dt(torch.empty(0, dtype=cd)), H_DIM):
+        pytest.skip("fused attention not built for this dtype")
+    g = torch.Generator(device=DEV).manual_seed(21)
+    q = torch.randn(N, Lq, 3 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)   # (Lq,N,3E)
+    kv = torch.randn(N, Lk, 2 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    o = torch.full((Lq, N, E), float("nan"), device=DEV, dtype=cd)
+    lse = torch.empty(N * Lq, device=DEV, dtype=torch.float32)
+    scale = 1.0 / math.sqrt(E)
+    qp, kp, vp = q[..., E:2 * E], kv[..., :E], kv[..., E:]
+    ops.attn_fwd(ops.dt(q), N, 1, Lq, Lk, E, qp.data_ptr(), (q.stride(0), q.stride(1)),
+                 kp.data_ptr(), (kv.stride(0), kv.stride(1)), vp.data_ptr(),
+                 (kv.stride(0), kv.stride(1)), o.data_ptr(), (o.stride(0), o.stride(1)), scale,
+                 lse)
+    torch.cuda.synchronize()
+    s = torch.einsum("lnd,knd->nlk", qp.float(), kp.float()) * scale
+    ref = torch.einsum("nlk,knd->lnd", torch.softmax(s, -1), vp.float())
+    err = (o.float() - ref).abs().max().item()
+    assert torch.isfinite(o.float()).all()
+    # P is rounded to the compute dtype before the PV product (as torch's 16-bit attention)
+    tol = (1e-2 if cd == torch.bfloat16 else 2e-3) * max(ref.abs().max().item(), 1.0)
+    assert err <= tol, err
+    lref = torch.logsumexp(s, -1).reshape(-1)
+    assert (lse - lref).abs().max().item() <= 1e-3 * max(lref.abs().max().item(), 1.0)
+
+
+def test_fused_attention_matches_unfused_path():
+    """AttnCoreFn with the fused kernel vs the GEMM + softmax path (JMT_ATTN_FUSED=0)."""
+    cd = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(22)
+    N, L, E = 4, 300, 512
+    x = torch.randn(N, L, 3 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    outs = []
+    for fused in (True, False):
+        ops._attn_fused["on"] = fused
+        try:
+            xx = x.detach().clone().requires_grad_(True)
+            with JF.compute_mode(cd):
+                o = JF.AttnCoreFn.apply(xx, xx, xx, E, 1, 0, E, 2 * E)
+            o.backward(torch.ones_like(o))
+            outs.append((o.float(), xx.grad.float()))
+        finally:
+            ops._attn_fused["on"] = True
+    (o1, g1), (o2, g2) = outs
+    assert (o1 - o2).abs().max().item() <= 1e-2 * o2.abs().max().item()
+    assert (g1 - g2).abs().max().item() <= 2e-2 * g2.abs().max().item()
