@@ -114,6 +114,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=64)
     ap.add_argument("--no-probe", action="store_true", help="no per-launch events (profiling)")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=True,
+                    help="replay the whole step as one hipGraph (default)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="eager launches from Python every step")
+    ap.add_argument("--probe-steps", type=int, default=3)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,6 +134,7 @@ def main():
     from jmt import ops
     from jmt import dist as jdist
     from jmt.optim import FusedSGD, used_parameters
+    from jmt.graph import GraphedStep
     from models.two_transformers import Two_transformers
     from models.fc_layer import FcLayer
     from losses.loss import CCCLoss
@@ -177,18 +183,32 @@ def main():
         return loss
 
     probe = GemmProbe((ops.dt(cd), True, True))
-    if not args.no_probe:
-        ops.set_launch_hook(probe)
     for _ in range(args.warmup):
         loss = step()
+    torch.cuda.synchronize()
+    # host issue time of one eager step (how long Python + autograd + ctypes take to enqueue it)
+    t_issue = time.perf_counter()
+    loss = step()
+    host_issue_ms = (time.perf_counter() - t_issue) * 1e3
+    torch.cuda.synchronize()
+
+    run = step
+    graphed = None
+    use_graph = args.graph and (world == 1 or os.environ.get("JMT_GRAPH_DIST", "0") == "1")
+    if use_graph:
+        # the whole step as one hipGraph (jmt/graph.py): replay issues ~300 launches at once
+        graphed = GraphedStep(step).capture(warmup=1)
+        run = graphed.replay
+    elif not args.no_probe:
+        ops.set_launch_hook(probe)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    probe.on = not args.no_probe
+    probe.on = not args.no_probe and not use_graph
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -196,6 +216,17 @@ def main():
     elapsed = time.perf_counter() - t0
     probe.on = False
     last_loss = float(loss)
+    if use_graph and not args.no_probe:
+        # per-launch HIP events cannot sit inside the replayed graph: the dominant kernel is
+        # timed over `probe_steps` eager steps right after the timed region, with the same
+        # stream concurrency, on the streams its launches go to
+        ops.set_launch_hook(probe)
+        probe.on = True
+        for _ in range(args.probe_steps):
+            step()
+        torch.cuda.synchronize()
+        probe.on = False
+        ops.set_launch_hook(None)
     if world > 1:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -212,7 +243,8 @@ def main():
                     "linears + attention scores)", "achieved": round(achieved, 1),
                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                    "launches_per_step": psum["launches"] // args.steps,
+                    "launches_per_step": psum["launches"] // (args.probe_steps if use_graph else args.steps),
+                    "timed_over": ("eager probe steps after the timed region" if use_graph else "the timed region"),
                     "avg_launch_us": round(psum["avg_ms"] * 1e3, 2),
                     "avg_gflop_per_launch": round(psum["avg_flops"] / 1e9, 3)}
     step_tf = step_flops(B, T) * world / (elapsed / args.steps) / 1e12
@@ -239,6 +271,8 @@ def main():
                           "frac_of_peak": round(step_tf / (PEAK_BF16_TFLOPS * world), 4)},
             "cpu_baseline": cpu,
             "final_loss": round(last_loss, 6),
+            "graph": bool(use_graph),
+            "host_issue_ms_per_eager_step": round(host_issue_ms, 3),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

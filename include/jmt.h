@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define JMT_ABI_VERSION 1
+#define JMT_ABI_VERSION 2
 
 enum { JMT_F32 = 0, JMT_BF16 = 1, JMT_F16 = 2 };
 enum { JMT_OK = 0, JMT_ERR_ARG = -1, JMT_ERR_HIP = -2, JMT_ERR_UNSUPPORTED = -3 };
@@ -72,6 +72,10 @@ typedef struct jmt_gemm_desc {
   int splits;
   void* workspace;
   size_t ws_bytes;
+  /* ABI 2: per-batch bias table (grouped GEMMs of several nn.Linear / in_proj modules in one
+   * launch): when n_bias > 0, batch b0 uses bias_tab[b0] (bias_mode 1 or 2) instead of bias. */
+  const float* bias_tab[8];
+  int n_bias;
 } jmt_gemm_desc;
 
 int jmt_gemm(const jmt_gemm_desc* desc, void* stream);

@@ -45,6 +45,8 @@ struct GemmParams {
   const void* b_ptr[MAXP];
   void* c_ptr[MAXP];
   const float* bias;
+  const float* bias_tab[MAXP];  // per-b0 bias vectors (n_bias > 0)
+  int n_bias;
   const void* aux;
   float* ws;
   int64_t lda, ldb, ldc, ldaux;
@@ -419,6 +421,7 @@ void gemm_kernel(GemmParams p) {
   // ---- epilogue.  acc[i][j] holds the TRANSPOSED 16x16 tile (the MFMA was fed B as its first
   //      operand): lane owns C row (lane&15) and the 4 consecutive columns 4*(lane>>4) + r.
   const bool partial = p.splits > 1;
+  const float* biasp = p.n_bias > 0 ? p.bias_tab[b0] : p.bias;
   O* cp;
   int64_t cbase;
   float alpha = p.alpha, beta = p.beta;
@@ -459,14 +462,14 @@ void gemm_kernel(GemmParams p) {
       const int n = n0 + wn * C::WTN + 16 * j + cq;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        bias4[j][e] = (bias_mode == 1 && n + e < p.N) ? p.bias[n + e] : 0.f;
+        bias4[j][e] = (bias_mode == 1 && n + e < p.N) ? biasp[n + e] : 0.f;
     }
     const bool plain = beta == 0.f && auxp == nullptr;
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
       const int m = m0 + wm * C::WTM + 16 * i + rl;
       if (m >= p.M) continue;
-      const float bm = (bias_mode == 2) ? p.bias[m] : 0.f;
+      const float bm = (bias_mode == 2) ? biasp[m] : 0.f;
       const int64_t rowo = cbase + (int64_t)m * ldc;
       const int64_t rowa = cbase + (int64_t)m * p.ldaux;
 #pragma unroll
@@ -536,6 +539,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
       }
     }
     const int b0 = b / p.batch1, b1 = b % p.batch1;
+    const float* biasp = p.n_bias > 0 ? p.bias_tab[b0] : p.bias;
     O* cp;
     int64_t cbase;
     if (p.c_mode == 1) {
@@ -551,8 +555,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
 #pragma unroll
     for (int i = 0; i < W; ++i) {
       float x = v[i] * p.alpha;
-      if (p.bias_mode == 1) x += p.bias[n + i];
-      else if (p.bias_mode == 2) x += p.bias[m];
+      if (p.bias_mode == 1) x += biasp[n + i];
+      else if (p.bias_mode == 2) x += biasp[m];
       if (p.beta != 0.f) x += p.beta * to_f(cp[co + i]);
       if (p.relu) x = fmaxf(x, 0.f);
       if (auxp && !(to_f(auxp[cbase + (int64_t)m * p.ldaux + n + i]) > 0.f)) x = 0.f;
@@ -717,7 +721,12 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
     p.b_ptr[i] = i < d->n_b ? d->b[i] : nullptr;
     p.c_ptr[i] = i < d->n_c ? d->c[i] : nullptr;
   }
+  JMT_CHECK_ARG(d->n_bias >= 0 && d->n_bias <= MAXP, "jmt_gemm: bias table size");
+  if (d->n_bias > 0)
+    JMT_CHECK_ARG(d->n_bias >= batch0 && d->bias_mode != 0, "jmt_gemm: bias table < batch0");
   p.bias = d->bias;
+  p.n_bias = d->n_bias;
+  for (int i = 0; i < MAXP; ++i) p.bias_tab[i] = i < d->n_bias ? d->bias_tab[i] : nullptr;
   p.aux = d->aux;
   p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc; p.ldaux = d->ldaux;
   p.sA0 = d->sA0; p.sA1 = d->sA1; p.sB0 = d->sB0; p.sB1 = d->sB1; p.sC0 = d->sC0; p.sC1 = d->sC1;
@@ -727,7 +736,7 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   p.M = d->M; p.N = d->N; p.K = d->K;
   p.batch0 = batch0; p.batch1 = batch1;
   p.alpha = d->alpha; p.beta = d->beta;
-  p.bias_mode = d->bias ? d->bias_mode : 0;
+  p.bias_mode = (d->bias || d->n_bias > 0) ? d->bias_mode : 0;
   p.relu = d->relu;
   p.c_dtype = d->c_dtype;
   p.aux_dtype = d->aux_dtype;

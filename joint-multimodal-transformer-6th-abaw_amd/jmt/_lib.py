@@ -38,6 +38,7 @@ class GemmDesc(C.Structure):
         ("aux", c_vp),
         ("splits", c_int),
         ("workspace", c_vp), ("ws_bytes", C.c_size_t),
+        ("bias_tab", c_vp * 8), ("n_bias", c_int),
     ]
 
 
@@ -107,7 +108,7 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.jmt_abi_version() != 1:
+    if lib.jmt_abi_version() != 2:
         raise JMTError("libjmt_hip.so ABI version mismatch")
     cfg = int(os.environ.get("JMT_GEMM_CFG", "0"))   # development: force a GEMM pipeline config
     if cfg:

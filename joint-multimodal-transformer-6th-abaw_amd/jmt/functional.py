@@ -22,6 +22,7 @@ import torch
 from torch.autograd import Function
 
 from . import ops
+from . import streams
 from ._lib import F32
 
 # ------------------------------------------------------------------------- precision policy
@@ -83,6 +84,7 @@ def register_shadow(w: torch.Tensor, shadow: torch.Tensor):
 def _grad_buffer(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     if p is None or not p.requires_grad:
         return None
+    streams.join_after_backward()
     if p.grad is None:
         p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
     return p.grad
@@ -443,109 +445,126 @@ class AttnCoreFn(Function):
 
     @staticmethod
     def forward(ctx, q_src, k_src, v_src, E, H, qcol, kcol, vcol):
-        cd = compute_dtype()
-        for t in (q_src, k_src, v_src):
-            assert t.dtype == cd and t.stride(-1) == 1
-        Lq, N = q_src.shape[0], q_src.shape[1]
-        Lk = k_src.shape[0]
-        dh = E // H
-        dev = q_src.device
-        ldS = _round_up(Lk, 8)
-        bS = (H * Lq * ldS, Lq * ldS)
-        scale = 1.0 / math.sqrt(dh)
-        o = Rows(q_src).like(E, cd)
-        fused = cd != torch.float32 and ops.attn_supported(_dc(cd), dh)
-        if fused:
-            # one kernel: scores stay on chip (attn.hip); the unnormalised probabilities, the
-            # per-tile maxima and the lse are kept for the fused backward
-            lse = torch.empty(N * H * Lq, dtype=torch.float32, device=dev)
-            P = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
-            mt = torch.empty(max(ops.attn_mt_floats(N, H, Lq, Lk), 1), dtype=torch.float32,
-                             device=dev)
-            ops.attn_fwd(_dc(cd), N, H, Lq, Lk, dh,
-                         _ptr(q_src, qcol), (q_src.stride(0), q_src.stride(1)),
-                         _ptr(k_src, kcol), (k_src.stride(0), k_src.stride(1)),
-                         _ptr(v_src, vcol), (v_src.stride(0), v_src.stride(1)),
-                         o.data_ptr(), (o.stride(0), o.stride(1)), scale, lse, P, ldS, mt)
-            ctx.save_for_backward(q_src, k_src, v_src, P, o, lse, mt)
-        else:
-            P = AttnCoreFn._probs(q_src, k_src, E, H, qcol, kcol, ldS, scale, cd)
-            ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
-                     a=[P.data_ptr()], lda=ldS, a_kmajor=True, sA=bS,
-                     b=[_ptr(v_src, vcol)], ldb=v_src.stride(0), b_kmajor=False,
-                     sB=(v_src.stride(1), dh),
-                     c=[o.data_ptr()], ldc=o.stride(0), sC=(o.stride(1), dh),
-                     batch0=N, batch1=H, device=dev)
-            ctx.save_for_backward(q_src, k_src, v_src, P, None, None, None)
+        o, saved = attn_forward(q_src, k_src, v_src, E, H, qcol, kcol, vcol)
         # which inputs are the same tensor (saved tensors are not guaranteed to unpack to the
         # same Python objects, so the aliasing is recorded here)
         owner = (0, 0 if k_src is q_src else 1,
                  0 if v_src is q_src else (1 if v_src is k_src else 2))
-        ctx.meta = (E, H, qcol, kcol, vcol, ldS, scale, cd, owner, fused)
+        ctx.save_for_backward(*saved[0])
+        ctx.meta = (saved[1], owner)
         return o
 
     @staticmethod
     def backward(ctx, go):
-        q_src, k_src, v_src, P, o, lse, mt = ctx.saved_tensors
-        E, H, qcol, kcol, vcol, ldS, scale, cd, owner, fused = ctx.meta
-        Lq, N = q_src.shape[0], q_src.shape[1]
-        Lk = k_src.shape[0]
-        dh = E // H
-        dev = q_src.device
-        v8 = _vec(cd)
-        if go.dtype != cd or go.stride(-1) != 1 or go.stride(0) % v8 or go.stride(1) % v8:
-            go = _cast_keep_layout(go if go.stride(-1) == 1 else go.contiguous(), cd)
-        sq_l, sq_n = q_src.stride(0), q_src.stride(1)
-        sk_l, sk_n = k_src.stride(0), k_src.stride(1)
-        sv_l, sv_n = v_src.stride(0), v_src.stride(1)
-        so_l, so_n = go.stride(0), go.stride(1)
-        if fused and go.data_ptr() % 16:
-            go = go.clone(memory_format=torch.contiguous_format)
-            so_l, so_n = go.stride(0), go.stride(1)
-        bS = (H * Lq * ldS, Lq * ldS)
+        tensors = ctx.saved_tensors
+        meta, owner = ctx.meta
+        q_src, k_src, v_src = tensors[:3]
+        cd = meta[7]
         # one gradient buffer per distinct source tensor (packed qkv -> one buffer)
         srcs = (q_src, k_src, v_src)
         bufs = [None, None, None]
         for i in range(3):
             if owner[i] == i:
                 bufs[i] = Rows(srcs[i]).like(srcs[i].shape[-1], cd)
-        dq, dk, dv = bufs[owner[0]], bufs[owner[1]], bufs[owner[2]]
-        dS = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
-        if fused:
-            # dP, softmax backward and dQ = dS K in one kernel; P normalised in place
-            ops.attn_bwd_dq(_dc(cd), N, H, Lq, Lk, dh, go.data_ptr(), (so_l, so_n),
-                            o.data_ptr(), (o.stride(0), o.stride(1)),
-                            _ptr(k_src, kcol), (sk_l, sk_n), _ptr(v_src, vcol), (sv_l, sv_n),
-                            lse, P, mt, ldS, dS, _ptr(dq, qcol), (dq.stride(0), dq.stride(1)),
-                            scale)
-        else:
-            dP = torch.empty(N * H * Lq * ldS, dtype=torch.float32, device=dev)
-            ops.gemm(M=Lq, N=Lk, K=dh, ab_dtype=_dc(cd), c_dtype=F32,
-                     a=[go.data_ptr()], lda=so_l, a_kmajor=True, sA=(so_n, dh),
-                     b=[_ptr(v_src, vcol)], ldb=sv_l, b_kmajor=True, sB=(sv_n, dh),
-                     c=[dP.data_ptr()], ldc=ldS, sC=bS, batch0=N, batch1=H, device=dev)
-            ops.softmax_bwd(P, ldS, dP, ldS, N * H * Lq, Lk, scale, dS, ldS)
-            del dP
-            # dQ = dS K
-            ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
-                     a=[dS.data_ptr()], lda=ldS, a_kmajor=True, sA=bS,
-                     b=[_ptr(k_src, kcol)], ldb=sk_l, b_kmajor=False, sB=(sk_n, dh),
-                     c=[_ptr(dq, qcol)], ldc=dq.stride(0), sC=(dq.stride(1), dh), batch0=N,
-                     batch1=H, device=dev)
-        # dK = dS^T Q
-        ops.gemm(M=Lk, N=dh, K=Lq, ab_dtype=_dc(cd), c_dtype=_dc(cd),
-                 a=[dS.data_ptr()], lda=ldS, a_kmajor=False, sA=bS,
-                 b=[_ptr(q_src, qcol)], ldb=sq_l, b_kmajor=False, sB=(sq_n, dh),
-                 c=[_ptr(dk, kcol)], ldc=dk.stride(0), sC=(dk.stride(1), dh), batch0=N,
-                 batch1=H, device=dev)
-        # dV = P^T dO
-        ops.gemm(M=Lk, N=dh, K=Lq, ab_dtype=_dc(cd), c_dtype=_dc(cd),
-                 a=[P.data_ptr()], lda=ldS, a_kmajor=False, sA=bS,
-                 b=[go.data_ptr()], ldb=so_l, b_kmajor=False, sB=(so_n, dh),
-                 c=[_ptr(dv, vcol)], ldc=dv.stride(0), sC=(dv.stride(1), dh), batch0=N,
-                 batch1=H, device=dev)
+        attn_backward((tensors, meta), go, bufs[owner[0]], bufs[owner[1]], bufs[owner[2]])
         grads = [bufs[i] if owner[i] == i else None for i in range(3)]
         return (*grads, None, None, None, None, None)
+
+
+def attn_forward(q_src, k_src, v_src, E, H, qcol, kcol, vcol):
+    """softmax(Q K^T / sqrt(dh)) V on seq-first strided views (see AttnCoreFn).  Returns the
+    output (Lq, N, E) (memory order of q_src's rows) and the state attn_backward needs."""
+    cd = compute_dtype()
+    for t in (q_src, k_src, v_src):
+        assert t.dtype == cd and t.stride(-1) == 1
+    Lq, N = q_src.shape[0], q_src.shape[1]
+    Lk = k_src.shape[0]
+    dh = E // H
+    dev = q_src.device
+    ldS = _round_up(Lk, 8)
+    bS = (H * Lq * ldS, Lq * ldS)
+    scale = 1.0 / math.sqrt(dh)
+    o = Rows(q_src).like(E, cd)
+    fused = cd != torch.float32 and ops.attn_supported(_dc(cd), dh)
+    if fused:
+        # one kernel: scores stay on chip (attn.hip); the unnormalised probabilities, the
+        # per-tile maxima and the lse are kept for the fused backward
+        lse = torch.empty(N * H * Lq, dtype=torch.float32, device=dev)
+        P = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
+        mt = torch.empty(max(ops.attn_mt_floats(N, H, Lq, Lk), 1), dtype=torch.float32,
+                         device=dev)
+        ops.attn_fwd(_dc(cd), N, H, Lq, Lk, dh,
+                     _ptr(q_src, qcol), (q_src.stride(0), q_src.stride(1)),
+                     _ptr(k_src, kcol), (k_src.stride(0), k_src.stride(1)),
+                     _ptr(v_src, vcol), (v_src.stride(0), v_src.stride(1)),
+                     o.data_ptr(), (o.stride(0), o.stride(1)), scale, lse, P, ldS, mt)
+        tensors = (q_src, k_src, v_src, P, o, lse, mt)
+    else:
+        P = AttnCoreFn._probs(q_src, k_src, E, H, qcol, kcol, ldS, scale, cd)
+        ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                 a=[P.data_ptr()], lda=ldS, a_kmajor=True, sA=bS,
+                 b=[_ptr(v_src, vcol)], ldb=v_src.stride(0), b_kmajor=False,
+                 sB=(v_src.stride(1), dh),
+                 c=[o.data_ptr()], ldc=o.stride(0), sC=(o.stride(1), dh),
+                 batch0=N, batch1=H, device=dev)
+        tensors = (q_src, k_src, v_src, P, None, None, None)
+    return o, (tensors, (E, H, qcol, kcol, vcol, ldS, scale, cd, fused))
+
+
+def attn_backward(saved, go, dq, dk, dv):
+    """Gradients of attn_forward written into dq / dk / dv (seq-first views laid out like the
+    sources; the same qcol/kcol/vcol column offsets; dq/dk/dv may be the same packed buffer)."""
+    (q_src, k_src, v_src, P, o, lse, mt), meta = saved
+    E, H, qcol, kcol, vcol, ldS, scale, cd, fused = meta
+    Lq, N = q_src.shape[0], q_src.shape[1]
+    Lk = k_src.shape[0]
+    dh = E // H
+    dev = q_src.device
+    v8 = _vec(cd)
+    if go.dtype != cd or go.stride(-1) != 1 or go.stride(0) % v8 or go.stride(1) % v8:
+        go = _cast_keep_layout(go if go.stride(-1) == 1 else go.contiguous(), cd)
+    sq_l, sq_n = q_src.stride(0), q_src.stride(1)
+    sk_l, sk_n = k_src.stride(0), k_src.stride(1)
+    sv_l, sv_n = v_src.stride(0), v_src.stride(1)
+    so_l, so_n = go.stride(0), go.stride(1)
+    if fused and go.data_ptr() % 16:
+        go = go.clone(memory_format=torch.contiguous_format)
+        so_l, so_n = go.stride(0), go.stride(1)
+    bS = (H * Lq * ldS, Lq * ldS)
+    dS = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
+    if fused:
+        # dP, softmax backward and dQ = dS K in one kernel; P normalised in place
+        ops.attn_bwd_dq(_dc(cd), N, H, Lq, Lk, dh, go.data_ptr(), (so_l, so_n),
+                        o.data_ptr(), (o.stride(0), o.stride(1)),
+                        _ptr(k_src, kcol), (sk_l, sk_n), _ptr(v_src, vcol), (sv_l, sv_n),
+                        lse, P, mt, ldS, dS, _ptr(dq, qcol), (dq.stride(0), dq.stride(1)),
+                        scale)
+    else:
+        dP = torch.empty(N * H * Lq * ldS, dtype=torch.float32, device=dev)
+        ops.gemm(M=Lq, N=Lk, K=dh, ab_dtype=_dc(cd), c_dtype=F32,
+                 a=[go.data_ptr()], lda=so_l, a_kmajor=True, sA=(so_n, dh),
+                 b=[_ptr(v_src, vcol)], ldb=sv_l, b_kmajor=True, sB=(sv_n, dh),
+                 c=[dP.data_ptr()], ldc=ldS, sC=bS, batch0=N, batch1=H, device=dev)
+        ops.softmax_bwd(P, ldS, dP, ldS, N * H * Lq, Lk, scale, dS, ldS)
+        del dP
+        # dQ = dS K
+        ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                 a=[dS.data_ptr()], lda=ldS, a_kmajor=True, sA=bS,
+                 b=[_ptr(k_src, kcol)], ldb=sk_l, b_kmajor=False, sB=(sk_n, dh),
+                 c=[_ptr(dq, qcol)], ldc=dq.stride(0), sC=(dq.stride(1), dh), batch0=N,
+                 batch1=H, device=dev)
+    # dK = dS^T Q
+    ops.gemm(M=Lk, N=dh, K=Lq, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+             a=[dS.data_ptr()], lda=ldS, a_kmajor=False, sA=bS,
+             b=[_ptr(q_src, qcol)], ldb=sq_l, b_kmajor=False, sB=(sq_n, dh),
+             c=[_ptr(dk, kcol)], ldc=dk.stride(0), sC=(dk.stride(1), dh), batch0=N,
+             batch1=H, device=dev)
+    # dV = P^T dO
+    ops.gemm(M=Lk, N=dh, K=Lq, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+             a=[P.data_ptr()], lda=ldS, a_kmajor=False, sA=bS,
+             b=[go.data_ptr()], ldb=so_l, b_kmajor=False, sB=(so_n, dh),
+             c=[_ptr(dv, vcol)], ldc=dv.stride(0), sC=(dv.stride(1), dh), batch0=N,
+             batch1=H, device=dev)
 
 
 def multihead_attention(query, key, value, in_w, in_b, out_w, out_b, num_heads):

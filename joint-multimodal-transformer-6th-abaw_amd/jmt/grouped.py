@@ -1,0 +1,438 @@
+"""Grouped execution of the JMT block's parallel branches (MultimodalTransformer_w_JR,
+mm_multi_transformers.py:118-214): the three encoders and the six cross-attentions run as
+batched launches instead of 3 / 6 separate ones.
+
+The reference applies three same-shaped TransformerEncoderLayers to v, a and the joint
+representation (:132-136), then three nn.MultiheadAttention modules twice each (:142-167), then
+`out_layer1` to the concatenation of the six outputs (:201-211).  Here the three encoder inputs
+live in ONE stacked buffer X (3, B, T, E); every GEMM of the three encoders is one launch whose
+per-batch operands come from pointer tables (weights, biases, gradient buffers: each module keeps
+its own nn.Parameters, so state_dict keys are untouched), the attention core runs over 3B
+sequences in one launch, and the six cross-attentions likewise over 6 stacked (query, key) pairs.
+The backward of each group is written out explicitly: gradients that the reference's autograd
+would sum from several uses (a stream's encoder output feeds 4 projections) are produced by ONE
+K-concatenated dgrad GEMM per stream (K = 6E), and weight gradients are accumulated in place
+(beta = 1) by batched wgrad GEMMs — no autograd adds, no cross-stream synchronisation, and a
+single HIP stream that captures into a hipGraph (jmt/graph.py).
+
+Stacked layouts (compute dtype, row-major, rows in (b, t) order per group):
+  X, Y   (G, B, T, E)     encoder group input / output            G = 3
+  QKV    (G', B, T, 3E)   packed in-projection outputs            G' = 3 (encoders), 6 (pairs)
+  O      (G', B, T, E)    attention outputs (before out_proj)
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Sequence
+
+import torch
+from torch.autograd import Function
+
+from . import ops
+from .functional import (_dc, _grad_buffer, _ptr, attn_backward, attn_forward, compute_dtype,
+                         weight_as)
+
+_enabled = {"on": os.environ.get("JMT_GROUPED", "1") != "0"}
+
+# the six cross-attentions in the reference's order (mm_multi_transformers.py:142-167), which is
+# also the order of torch.cat in the FC head (:201-211): (module, query stream, key/value stream)
+# with module 0 = cross_attention_v, 1 = cross_attention_p, 2 = cross_attention_pv and stream
+# 0 = visual, 1 = physiological (audio), 2 = joint representation.
+CROSS_PAIRS = ((0, 0, 1), (1, 1, 0), (2, 2, 0), (0, 0, 2), (2, 2, 1), (1, 1, 2))
+
+
+def enabled() -> bool:
+    return _enabled["on"]
+
+
+def set_enabled(on: bool) -> None:
+    _enabled["on"] = bool(on)
+
+
+# ------------------------------------------------------------------------- grouped GEMMs
+def _gemm_fwd(a_ptrs: Sequence[int], lda: int, sA: int, rows: int, K: int, Ws, r0: int, n: int,
+              bs, c_ptr: int, ldc: int, sC: int, c_dt: int, cd, dev, relu: bool = False):
+    """C[g] = A[g] (rows x K) . W_g[r0:r0+n]^T + b_g[r0:r0+n]  for g < len(Ws), one launch.
+    A is strided (a_ptrs = [base], sA) or a per-group pointer table (len(a_ptrs) == len(Ws))."""
+    Wc = [weight_as(W, cd) for W in Ws]
+    Kin = Wc[0].shape[1]
+    table = len(a_ptrs) > 1
+    ops.gemm(M=rows, N=n, K=K, ab_dtype=_dc(cd), c_dtype=c_dt,
+             a=list(a_ptrs), lda=lda, a_kmajor=True, a_mode=1 if table else 0,
+             sA=(0 if table else sA, 0),
+             b=[_ptr(w, r0 * Kin) for w in Wc], ldb=Kin, b_kmajor=True, b_mode=1,
+             c=[c_ptr], ldc=ldc, sC=(sC, 0), batch0=len(Ws),
+             bias_tab=[b[r0:r0 + n] for b in bs] if bs is not None else None, bias_mode=1,
+             relu=relu, device=dev)
+
+
+def _gemm_dgrad(dy_ptr: int, ldy: int, sdy: int, rows: int, n: int, Ws, r0: int, c_ptr: int,
+                ldc: int, sC: int, c_dt: int, cd, dev, beta: float = 0.0, aux=None,
+                ldaux: int = 0):
+    """dX[g] (+)= dY[g] (rows x n) . W_g[r0:r0+n, :]  (masked by aux > 0: ReLU backward)."""
+    Wc = [weight_as(W, cd) for W in Ws]
+    Kin = Wc[0].shape[1]
+    ops.gemm(M=rows, N=Kin, K=n, ab_dtype=_dc(cd), c_dtype=c_dt,
+             a=[dy_ptr], lda=ldy, a_kmajor=True, sA=(sdy, 0),
+             b=[_ptr(w, r0 * Kin) for w in Wc], ldb=Kin, b_kmajor=False, b_mode=1,
+             c=[c_ptr], ldc=ldc, sC=(sC, 0), batch0=len(Ws), beta=beta,
+             aux=aux, ldaux=ldaux, device=dev)
+
+
+def _gemm_wgrad(dy_ptrs: Sequence[int], ldy: int, sdy: int, x_ptrs: Sequence[int], ldx: int,
+                sx: int, rows: int, n: int, Ws, r0: int, cd, dev):
+    """W_g.grad[r0:r0+n] += dY[g]^T X[g]  (fp32, split-K over the rows).  dY / X are strided
+    ([base], stride) or per-group pointer tables.  The Ws of one launch must be distinct
+    parameters (their gradient regions are written concurrently)."""
+    grads = []
+    for W in Ws:
+        g = _grad_buffer(W)
+        grads.append(g if g is not None else torch.zeros_like(W))
+    Kin = Ws[0].shape[1]
+    ta, tb = len(dy_ptrs) > 1, len(x_ptrs) > 1
+    ops.gemm(M=n, N=Kin, K=rows, ab_dtype=_dc(cd), c_dtype=ops.F32,
+             a=list(dy_ptrs), lda=ldy, a_kmajor=False, a_mode=1 if ta else 0,
+             sA=(0 if ta else sdy, 0),
+             b=list(x_ptrs), ldb=ldx, b_kmajor=False, b_mode=1 if tb else 0,
+             sB=(0 if tb else sx, 0),
+             c=[_ptr(g, r0 * Kin) for g in grads], ldc=Kin, c_mode=1, batch0=len(Ws),
+             beta=1.0, device=dev)
+
+
+def _bias_grad(dy2: torch.Tensor, ld: int, rows: int, n: int, b, r0: int):
+    gb = _grad_buffer(b)
+    if gb is not None:
+        ops.colsum(dy2, ld, rows, n, gb[r0:r0 + n], beta_acc=True)
+
+
+def _contig(t: torch.Tensor, cd) -> torch.Tensor:
+    if t.dtype != cd:
+        t = ops.cast(t.contiguous(), cd)
+    return t if t.is_contiguous() else t.contiguous()
+
+
+# ------------------------------------------------------------------------- stacking
+class StackGroupsFn(Function):
+    """X = stack(xs) -> (G, B, T, E) in the compute dtype (one strided copy per stream); the
+    backward hands out views of the incoming gradient."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        cd = compute_dtype()
+        x0 = xs[0]
+        B, T, E = x0.shape
+        X = torch.empty(len(xs), B, T, E, dtype=cd, device=x0.device)
+        for g, x in enumerate(xs):
+            assert tuple(x.shape) == (B, T, E), "StackGroupsFn: streams must share (B, T, E)"
+            if x.stride(-1) != 1 or x.stride(1) != E * x.stride(2) or x.stride(0) != T * x.stride(1):
+                x = x.contiguous()
+            ops.copy2d(x.data_ptr(), ops.dt(x), X[g].data_ptr(), ops.dt(X), B * T, E,
+                       x.stride(1), 1, E, 1)
+        return X
+
+    @staticmethod
+    def backward(ctx, dX):
+        return tuple(dX[g] for g in range(dX.shape[0]))
+
+
+def stack_groups(*xs) -> torch.Tensor:
+    return StackGroupsFn.apply(*xs)
+
+
+# ------------------------------------------------------------------------- encoder group
+def encoder_layer_params(layer) -> List[torch.Tensor]:
+    """The 12 parameters of one TransformerEncoderLayer (mm_multi_transformers.py:48-70)."""
+    a, ff = layer.attention, layer.feed_forward
+    return [a.in_proj_weight, a.in_proj_bias, a.out_proj.weight, a.out_proj.bias,
+            ff[0].weight, ff[0].bias, ff[len(ff) - 1].weight, ff[len(ff) - 1].bias,
+            layer.layer_norm1.weight, layer.layer_norm1.bias,
+            layer.layer_norm2.weight, layer.layer_norm2.bias]
+
+
+class EncoderGroupFn(Function):
+    """G post-LN encoder layers (mm_multi_transformers.py:61-70, one per stream, same shapes,
+    own weights) on the stacked seq-first input X (G, B, T, E):
+        Y_g = LN2(H_g + W2 relu(W1 H_g + b1) + b2),  H_g = LN1(X_g + MHA_g(X_g, X_g, X_g)).
+    params: 12 per group (encoder_layer_params)."""
+
+    @staticmethod
+    def forward(ctx, X, meta, *params):
+        H, eps1, eps2 = meta
+        cd = compute_dtype()
+        X = _contig(X, cd)
+        G, B, T, E = X.shape
+        R = B * T
+        dev = X.device
+        P = [params[12 * g:12 * g + 12] for g in range(G)]
+        hid = P[0][4].shape[0]
+        cdt = _dc(cd)
+        # packed in-projection (3 groups, one launch)
+        QKV = torch.empty(G, B, T, 3 * E, dtype=cd, device=dev)
+        _gemm_fwd([X.data_ptr()], E, R * E, R, E, [p[0] for p in P], 0, 3 * E,
+                  [p[1] for p in P], QKV.data_ptr(), 3 * E, R * 3 * E, cdt, cd, dev)
+        sf = QKV.view(G * B, T, 3 * E).permute(1, 0, 2)          # (T, G*B, 3E) seq-first
+        o, asaved = attn_forward(sf, sf, sf, E, H, 0, E, 2 * E)  # memory (G*B, T, E)
+        O = o.permute(1, 0, 2)
+        A1 = torch.empty(G, B, T, E, dtype=cd, device=dev)
+        _gemm_fwd([O.data_ptr()], E, R * E, R, E, [p[2] for p in P], 0, E, [p[3] for p in P],
+                  A1.data_ptr(), E, R * E, cdt, cd, dev)
+        H1 = torch.empty_like(A1)
+        st1 = torch.empty(2, G * R, dtype=torch.float32, device=dev)
+        for g in range(G):
+            ops.layernorm_fwd(X[g], E, A1[g], E, P[g][8], P[g][9], eps1, H1[g], E,
+                              st1[0, g * R:], st1[1, g * R:], R, E)
+        F1 = torch.empty(G, B, T, hid, dtype=cd, device=dev)
+        _gemm_fwd([H1.data_ptr()], E, R * E, R, E, [p[4] for p in P], 0, hid,
+                  [p[5] for p in P], F1.data_ptr(), hid, R * hid, cdt, cd, dev, relu=True)
+        F2 = torch.empty(G, B, T, E, dtype=cd, device=dev)
+        _gemm_fwd([F1.data_ptr()], hid, R * hid, R, hid, [p[6] for p in P], 0, E,
+                  [p[7] for p in P], F2.data_ptr(), E, R * E, cdt, cd, dev)
+        Y = torch.empty_like(A1)
+        st2 = torch.empty(2, G * R, dtype=torch.float32, device=dev)
+        for g in range(G):
+            ops.layernorm_fwd(H1[g], E, F2[g], E, P[g][10], P[g][11], eps2, Y[g], E,
+                              st2[0, g * R:], st2[1, g * R:], R, E)
+        ctx.params = params
+        ctx.state = (X, QKV, asaved, O, A1, H1, st1, F1, F2, st2)
+        ctx.meta = (G, B, T, E, hid, cd)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        G, B, T, E, hid, cd = ctx.meta
+        X, QKV, asaved, O, A1, H1, st1, F1, F2, st2 = ctx.state
+        params = ctx.params
+        P = [params[12 * g:12 * g + 12] for g in range(G)]
+        R = B * T
+        dev = X.device
+        cdt = _dc(cd)
+        dY = _contig(dY, cd)
+
+        def ln_bwd(x, r, dy, st, gamma, beta, dx):
+            for g in range(G):
+                dgam = _grad_buffer(gamma[g])
+                dbet = _grad_buffer(beta[g])
+                tmp = None
+                if dgam is None or dbet is None:
+                    tmp = torch.empty(2, E, dtype=torch.float32, device=dev)
+                ops.layernorm_bwd(x[g], E, r[g], E, dy[g], E, st[0, g * R:], st[1, g * R:],
+                                  gamma[g], dx[g], E, dgam if dgam is not None else tmp[0],
+                                  dbet if dbet is not None else tmp[1], tmp is None, R, E)
+
+        # LN2: dS2 = d(H1 + F2)
+        dS = torch.empty(G, B, T, E, dtype=cd, device=dev)
+        ln_bwd(H1, F2, dY, st2, [p[10] for p in P], [p[11] for p in P], dS)
+        # FFN (the ReLU mask is fused into the W2 dgrad epilogue)
+        dF1 = torch.empty(G, B, T, hid, dtype=cd, device=dev)
+        _gemm_dgrad(dS.data_ptr(), E, R * E, R, E, [p[6] for p in P], 0, dF1.data_ptr(), hid,
+                    R * hid, cdt, cd, dev, aux=F1, ldaux=hid)
+        _gemm_wgrad([dS.data_ptr()], E, R * E, [F1.data_ptr()], hid, R * hid, R, E,
+                    [p[6] for p in P], 0, cd, dev)
+        for g in range(G):
+            _bias_grad(dS[g], E, R, E, P[g][7], 0)
+        # dH1 = dS2 + dF1 . W1  (in place on dS: beta = 1)
+        _gemm_dgrad(dF1.data_ptr(), hid, R * hid, R, hid, [p[4] for p in P], 0, dS.data_ptr(),
+                    E, R * E, cdt, cd, dev, beta=1.0)
+        _gemm_wgrad([dF1.data_ptr()], hid, R * hid, [H1.data_ptr()], E, R * E, R, hid,
+                    [p[4] for p in P], 0, cd, dev)
+        for g in range(G):
+            _bias_grad(dF1[g], hid, R, hid, P[g][5], 0)
+        # LN1: dS1 = d(X + A1)
+        dS1 = torch.empty_like(dS)
+        ln_bwd(X, A1, dS, st1, [p[8] for p in P], [p[9] for p in P], dS1)
+        # out_proj
+        dO = dS     # reuse: dS is dead
+        _gemm_dgrad(dS1.data_ptr(), E, R * E, R, E, [p[2] for p in P], 0, dO.data_ptr(), E,
+                    R * E, cdt, cd, dev)
+        _gemm_wgrad([dS1.data_ptr()], E, R * E, [O.data_ptr()], E, R * E, R, E,
+                    [p[2] for p in P], 0, cd, dev)
+        for g in range(G):
+            _bias_grad(dS1[g], E, R, E, P[g][3], 0)
+        # attention core -> packed dQKV
+        dQKV = torch.empty(G, B, T, 3 * E, dtype=cd, device=dev)
+        dsf = dQKV.view(G * B, T, 3 * E).permute(1, 0, 2)
+        attn_backward(asaved, dO.view(G * B, T, E).permute(1, 0, 2), dsf, dsf, dsf)
+        # in_proj: dX = dS1 + dQKV . W_in  (in place on dS1)
+        _gemm_dgrad(dQKV.data_ptr(), 3 * E, R * 3 * E, R, 3 * E, [p[0] for p in P], 0,
+                    dS1.data_ptr(), E, R * E, cdt, cd, dev, beta=1.0)
+        _gemm_wgrad([dQKV.data_ptr()], 3 * E, R * 3 * E, [X.data_ptr()], E, R * E, R, 3 * E,
+                    [p[0] for p in P], 0, cd, dev)
+        for g in range(G):
+            _bias_grad(dQKV[g], 3 * E, R, 3 * E, P[g][1], 0)
+        ctx.state = None
+        return (dS1, None) + (None,) * len(params)
+
+
+def encoder_group(X, layers, num_heads: int):
+    """Apply `layers` (one TransformerEncoderLayer per stream) to the stacked X."""
+    params = [p for layer in layers for p in encoder_layer_params(layer)]
+    meta = (num_heads, layers[0].layer_norm1.eps, layers[0].layer_norm2.eps)
+    return EncoderGroupFn.apply(X, meta, *params)
+
+
+# ------------------------------------------------------------------------- cross attentions
+def mha_params(mha) -> List[torch.Tensor]:
+    return [mha.in_proj_weight, mha.in_proj_bias, mha.out_proj.weight, mha.out_proj.bias]
+
+
+class CrossAttention6Fn(Function):
+    """The six key-is-value cross-attentions of mm_multi_transformers.py:142-167 on the stacked
+    encoder outputs Y (3, B, T, E) -> O6 (6, B, T, E) in the reference's concatenation order
+    (CROSS_PAIRS).  params: 4 per module (mha_params) for cross_attention_v / _p / _pv."""
+
+    @staticmethod
+    def forward(ctx, Y, meta, *params):
+        H, pairs = meta
+        cd = compute_dtype()
+        Y = _contig(Y, cd)
+        S, B, T, E = Y.shape
+        R = B * T
+        dev = Y.device
+        cdt = _dc(cd)
+        M = [params[4 * m:4 * m + 4] for m in range(len(params) // 4)]
+        NP = len(pairs)
+        QKV = torch.empty(NP, B, T, 3 * E, dtype=cd, device=dev)
+        in_w = [M[m][0] for m, _, _ in pairs]
+        in_b = [M[m][1] for m, _, _ in pairs]
+        # queries (each module's query projection is evaluated for both of its calls, exactly as
+        # the reference does) and packed key/values, one launch each
+        _gemm_fwd([Y[q].data_ptr() for _, q, _ in pairs], E, 0, R, E, in_w, 0, E, in_b,
+                  QKV.data_ptr(), 3 * E, R * 3 * E, cdt, cd, dev)
+        _gemm_fwd([Y[k].data_ptr() for _, _, k in pairs], E, 0, R, E, in_w, E, 2 * E, in_b,
+                  _ptr(QKV, E), 3 * E, R * 3 * E, cdt, cd, dev)
+        sf = QKV.view(NP * B, T, 3 * E).permute(1, 0, 2)
+        o, asaved = attn_forward(sf, sf, sf, E, H, 0, E, 2 * E)
+        O = o.permute(1, 0, 2)                                   # (NP*B, T, E) memory
+        O6 = torch.empty(NP, B, T, E, dtype=cd, device=dev)
+        _gemm_fwd([O.data_ptr()], E, R * E, R, E, [M[m][2] for m, _, _ in pairs], 0, E,
+                  [M[m][3] for m, _, _ in pairs], O6.data_ptr(), E, R * E, cdt, cd, dev)
+        ctx.params = params
+        ctx.state = (Y, QKV, asaved, O)
+        ctx.meta = (pairs, S, B, T, E, cd)
+        return O6
+
+    @staticmethod
+    def backward(ctx, dO6):
+        pairs, S, B, T, E, cd = ctx.meta
+        Y, QKV, asaved, O = ctx.state
+        params = ctx.params
+        M = [params[4 * m:4 * m + 4] for m in range(len(params) // 4)]
+        NP = len(pairs)
+        R = B * T
+        dev = Y.device
+        cdt = _dc(cd)
+        dO6 = _contig(dO6, cd)
+        # launches of the batched wgrads: each launch holds distinct modules
+        halves, seen = [[]], [set()]
+        for i, (m, _, _) in enumerate(pairs):
+            if m in seen[-1]:
+                halves.append([])
+                seen.append(set())
+            halves[-1].append(i)
+            seen[-1].add(m)
+        # out_proj
+        dO = torch.empty(NP, B, T, E, dtype=cd, device=dev)
+        _gemm_dgrad(dO6.data_ptr(), E, R * E, R, E, [M[m][2] for m, _, _ in pairs], 0,
+                    dO.data_ptr(), E, R * E, cdt, cd, dev)
+        for h in halves:
+            _gemm_wgrad([_ptr(dO6, i * R * E) for i in h], E, 0, [O[i * B].data_ptr() for i in h],
+                        E, 0, R, E, [M[pairs[i][0]][2] for i in h], 0, cd, dev)
+        for i, (m, _, _) in enumerate(pairs):
+            _bias_grad(dO6[i], E, R, E, M[m][3], 0)
+        # attention core -> packed dQKV (NP, B, T, 3E)
+        dQKV = torch.empty(NP, B, T, 3 * E, dtype=cd, device=dev)
+        dsf = dQKV.view(NP * B, T, 3 * E).permute(1, 0, 2)
+        attn_backward(asaved, dO.view(NP * B, T, E).permute(1, 0, 2), dsf, dsf, dsf)
+        # in_proj weight gradients: query rows [0, E) from the query stream, key/value rows
+        # [E, 3E) from the key stream
+        for h in halves:
+            ws = [M[pairs[i][0]][0] for i in h]
+            _gemm_wgrad([_ptr(dQKV, i * R * 3 * E) for i in h], 3 * E, 0,
+                        [Y[pairs[i][1]].data_ptr() for i in h], E, 0, R, E, ws, 0, cd, dev)
+            _gemm_wgrad([_ptr(dQKV, i * R * 3 * E + E) for i in h], 3 * E, 0,
+                        [Y[pairs[i][2]].data_ptr() for i in h], E, 0, R, 2 * E, ws, E, cd, dev)
+        for i, (m, _, _) in enumerate(pairs):
+            _bias_grad(dQKV[i], 3 * E, R, 3 * E, M[m][1], 0)
+        # stream gradients: every use of stream s (as a query: rows [0,E) of W_in; as a key /
+        # value: rows [E,2E) and [2E,3E)) is one K-segment of ONE dgrad GEMM (K = nseg * E)
+        dY = torch.zeros(S, B, T, E, dtype=cd, device=dev) if any(
+            not any(q == s or k == s for _, q, k in pairs) for s in range(S)) else \
+            torch.empty(S, B, T, E, dtype=cd, device=dev)
+        for s in range(S):
+            a_ptrs, b_ptrs = [], []
+            for i, (m, q, k) in enumerate(pairs):
+                Wc = weight_as(M[m][0], cd)
+                if q == s:
+                    a_ptrs.append(_ptr(dQKV, i * R * 3 * E))
+                    b_ptrs.append(_ptr(Wc, 0))
+                if k == s:
+                    a_ptrs += [_ptr(dQKV, i * R * 3 * E + E), _ptr(dQKV, i * R * 3 * E + 2 * E)]
+                    b_ptrs += [_ptr(Wc, E * E), _ptr(Wc, 2 * E * E)]
+            for c0 in range(0, len(a_ptrs), 8):   # at most 8 K-segments per launch
+                ap, bp = a_ptrs[c0:c0 + 8], b_ptrs[c0:c0 + 8]
+                ops.gemm(M=R, N=E, K=len(ap) * E, ab_dtype=cdt, c_dtype=cdt,
+                         a=ap, lda=3 * E, a_kmajor=True, a_mode=2, a_kseg=E,
+                         b=bp, ldb=E, b_kmajor=False, b_mode=2, b_kseg=E,
+                         c=[dY[s].data_ptr()], ldc=E, beta=1.0 if c0 else 0.0, device=dev)
+        ctx.state = None
+        return (dY, None) + (None,) * len(params)
+
+
+def cross_attention6(Y, modules, num_heads: int, pairs=CROSS_PAIRS):
+    params = [p for mod in modules for p in mha_params(mod)]
+    return CrossAttention6Fn.apply(Y, (num_heads, pairs), *params)
+
+
+# ------------------------------------------------------------------------- concat head
+class ConcatLinearFn(Function):
+    """y = cat(X[0], ..., X[S-1], dim=-1) . W^T + b for a stacked X (S, B, T, E): the FC head's
+    torch.cat + out_layer1 (mm_multi_transformers.py:201-211) as one K-concatenated GEMM; the
+    backward writes the stacked dX in one batched dgrad launch and W.grad in one batched wgrad."""
+
+    @staticmethod
+    def forward(ctx, X, W, b):
+        cd = compute_dtype()
+        X = _contig(X, cd)
+        S, B, T, E = X.shape
+        R = B * T
+        N = W.shape[0]
+        assert W.shape[1] == S * E
+        dev = X.device
+        Wc = weight_as(W, cd)
+        y = torch.empty(B, T, N, dtype=cd, device=dev)
+        ops.gemm(M=R, N=N, K=S * E, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                 a=[X[s].data_ptr() for s in range(S)], lda=E, a_kmajor=True, a_mode=2,
+                 a_kseg=E, b=[Wc.data_ptr()], ldb=S * E, b_kmajor=True,
+                 c=[y.data_ptr()], ldc=N, bias=b, bias_mode=1, device=dev)
+        ctx.save_for_backward(X, W, b)
+        ctx.meta = cd
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        X, W, b = ctx.saved_tensors
+        cd = ctx.meta
+        S, B, T, E = X.shape
+        R = B * T
+        N = W.shape[0]
+        dev = X.device
+        dy = _contig(dy, cd)
+        Wc = weight_as(W, cd)
+        dX = torch.empty_like(X)
+        ops.gemm(M=R, N=E, K=N, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                 a=[dy.data_ptr()], lda=N, a_kmajor=True, sA=(0, 0),
+                 b=[Wc.data_ptr()], ldb=S * E, b_kmajor=False, sB=(E, 0),
+                 c=[dX.data_ptr()], ldc=E, sC=(R * E, 0), batch0=S, device=dev)
+        gW = _grad_buffer(W)
+        if gW is not None:
+            ops.gemm(M=N, N=E, K=R, ab_dtype=_dc(cd), c_dtype=ops.F32,
+                     a=[dy.data_ptr()], lda=N, a_kmajor=False, sA=(0, 0),
+                     b=[X.data_ptr()], ldb=E, b_kmajor=False, sB=(R * E, 0),
+                     c=[gW.data_ptr()], ldc=S * E, sC=(E, 0), batch0=S, beta=1.0, device=dev)
+        if b is not None:
+            _bias_grad(dy, N, R, N, b, 0)
+        return dX, None, None
+
+
+def concat_linear(X, W, b):
+    return ConcatLinearFn.apply(X, W, b)

@@ -61,7 +61,7 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
          batch0: int = 1, batch1: int = 1, sA=(0, 0), sB=(0, 0), sC=(0, 0),
          alpha: float = 1.0, beta: float = 0.0, bias: Optional[torch.Tensor] = None,
          bias_mode: int = 1, relu: bool = False, aux: Optional[torch.Tensor] = None,
-         ldaux: int = 0, splits: Optional[int] = None, device=None) -> None:
+         ldaux: int = 0, splits: Optional[int] = None, bias_tab=None, device=None) -> None:
     d = GemmDesc()
     d.ab_dtype, d.c_dtype = ab_dtype, c_dtype
     d.aux_dtype = dt(aux) if aux is not None else c_dtype
@@ -83,7 +83,11 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
     d.sC0, d.sC1 = sC
     d.alpha, d.beta = alpha, beta
     d.bias = bias.data_ptr() if bias is not None else None
-    d.bias_mode = bias_mode if bias is not None else 0
+    d.bias_mode = bias_mode if (bias is not None or bias_tab) else 0
+    if bias_tab:
+        for i, t in enumerate(bias_tab):
+            d.bias_tab[i] = t.data_ptr()
+        d.n_bias = len(bias_tab)
     d.relu = int(relu)
     d.aux = aux.data_ptr() if aux is not None else None
     if splits is None:

@@ -9,6 +9,7 @@ import torch
 import torch.nn as nn
 
 from jmt import functional as F
+from jmt import grouped
 from jmt import streams
 from jmt.nn import Linear, LayerNorm, MLP, MultiheadAttention
 
@@ -110,6 +111,9 @@ class MultimodalTransformer_w_JR(nn.Module):
         # cat + out_layer_pv as ONE K-concatenated GEMM (:120-124)
         joint_representation = F.linear((visual_features, physiological_features),
                                         self.out_layer_pv.weight, self.out_layer_pv.bias)
+        if grouped.enabled() and visual_features.shape == physiological_features.shape:
+            return self._forward_grouped(visual_features, physiological_features,
+                                         joint_representation)
         v = visual_features.permute(1, 0, 2)          # free: a strided view (:127-129)
         p = physiological_features.permute(1, 0, 2)
         j = joint_representation.permute(1, 0, 2)
@@ -137,17 +141,36 @@ class MultimodalTransformer_w_JR(nn.Module):
                 r_pv[1],     # CA_pv(j, p)
                 r_p[1]]      # CA_p(p, j)
         if self.output_format == "SELF_ATTEN":
-            # :169-199 — stack to (6, B*T, 512), encoder over the 6-token sequences, MHA, keep
-            # token 5.  Only the last query row of the final attention is computed: it is the
-            # only one the reference keeps ([:, :, -1, :], :193).
-            T, B, E = outs[0].shape
-            st = F.stack_seq(outs, seq_first_in=True)
-            enc = self.final_visual_encoder(st)
-            last = enc[-1:]
-            fa, _ = self.final_self_attention(last, enc, enc)
-            return fa[0].reshape(B, T, E)
+            return self._self_atten_head(outs)
         # FC head (:201-211): torch.cat of the 6 outputs never materialised (K-concat GEMM)
         return F.linear(tuple(outs), self.out_layer1.weight, self.out_layer1.bias)
+
+    def _forward_grouped(self, visual_features, physiological_features, joint_representation):
+        """Same math, batched across the parallel branches (jmt/grouped.py): the three streams
+        in one stacked (3, B, T, E) buffer, each encoder layer of the three encoders as one
+        grouped launch sequence, the six cross-attentions as one (:132-167)."""
+        X = grouped.stack_groups(visual_features, physiological_features, joint_representation)
+        for lv, lp, lj in zip(self.visual_encoder.layers, self.physiological_encoder.layers,
+                              self.joint_representation_encoder.layers):
+            X = grouped.encoder_group(X, [lv, lp, lj], self.num_heads)
+        O6 = grouped.cross_attention6(X, [self.cross_attention_v, self.cross_attention_p,
+                                          self.cross_attention_pv], self.num_heads)
+        if self.output_format == "SELF_ATTEN":
+            return self._self_atten_head([O6[i].permute(1, 0, 2) for i in range(6)])
+        # FC head (:201-211): seq-first (T, B, 1024), as the reference returns it
+        return grouped.concat_linear(O6, self.out_layer1.weight,
+                                     self.out_layer1.bias).permute(1, 0, 2)
+
+    def _self_atten_head(self, outs):
+        # :169-199 — stack to (6, B*T, 512), encoder over the 6-token sequences, MHA, keep
+        # token 5.  Only the last query row of the final attention is computed: it is the
+        # only one the reference keeps ([:, :, -1, :], :193).
+        T, B, E = outs[0].shape
+        st = F.stack_seq(outs, seq_first_in=True)
+        enc = self.final_visual_encoder(st)
+        last = enc[-1:]
+        fa, _ = self.final_self_attention(last, enc, enc)
+        return fa[0].reshape(B, T, E)
 
 
 class FeatureConcatFC(nn.Module):
