@@ -155,6 +155,12 @@ int jmt_attn_bwd_dq(int dt, int N, int H, int Lq, int Lk, int dh, const void* go
 int jmt_colsum_blocks(int64_t rows);
 int jmt_colsum(int dt, int64_t rows, int N, const void* dy, int64_t ld, float* db, int beta_acc,
                float* partials, void* stream);
+/* G column sums in one launch pair (bias gradients of G same-shaped nn.Linear / in_proj modules
+ * run as one grouped GEMM): group g reads dy + g*sdy and reduces into db_tab[g] (G <= 8;
+ * partials: G * jmt_colsum_blocks(rows) * N floats; N, ld, sdy multiples of 16/elem bytes). */
+int jmt_colsum_grouped(int dt, int G, int64_t rows, int N, const void* dy, int64_t ld,
+                       int64_t sdy, float* const* db_tab, int beta_acc, float* partials,
+                       void* stream);
 
 /* Strided 2-D copy with dtype conversion and optional transpose (layout plumbing:
  * the (T,B) output of the FC head, torch.stack of the SELF_ATTEN head). dst may be accumulated

@@ -323,6 +323,26 @@ __device__ __forceinline__ void wait_tiles(int n) {
   }
 }
 
+// 4 consecutive elements row[n..n+3] as floats (one vector load when aligned and in range;
+// elements past `lim` read as 0)
+template <typename O>
+__device__ __forceinline__ void load4_guard(const O* row, int n, int lim, bool vec4, float (&v)[4]) {
+  if (vec4 && n + 4 <= lim) {
+    if constexpr (sizeof(O) == 4) {
+      const float4 t = *(const float4*)(row + n);
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+      const uint2 t = *(const uint2*)(row + n);
+      const O* h = (const O*)&t;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = to_f(h[e]);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (n + e < lim) ? to_f(row[n + e]) : 0.f;
+  }
+}
+
 // ------------------------------------------------------------------ main kernel
 template <typename T, typename O, bool AK, bool BK, class C>
 __global__ __launch_bounds__(C::NT, 2 * 256 / C::NT > 0 ? 2 * 256 / C::NT : 1)
@@ -472,6 +492,17 @@ void gemm_kernel(GemmParams p) {
       const float bm = (bias_mode == 2) ? biasp[m] : 0.f;
       const int64_t rowo = cbase + (int64_t)m * ldc;
       const int64_t rowa = cbase + (int64_t)m * p.ldaux;
+      // beta*C / ReLU-mask operands: all TN 4-element groups of this row are loaded up front
+      // (one 8-B / 16-B load each, uniform branches) so their latencies overlap
+      float cin[C::TN][4], ain[C::TN][4];
+      if (beta != 0.f) {
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j) load4_guard(cp + rowo, n0 + wn * C::WTN + 16 * j + cq, p.N, vec4, cin[j]);
+      }
+      if (auxp) {
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j) load4_guard(auxp + rowa, n0 + wn * C::WTN + 16 * j + cq, p.N, vec4, ain[j]);
+      }
 #pragma unroll
       for (int j = 0; j < C::TN; ++j) {
         const int n = n0 + wn * C::WTN + 16 * j + cq;
@@ -483,11 +514,9 @@ void gemm_kernel(GemmParams p) {
         if (!plain) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            if (n + e < p.N) {
-              if (beta != 0.f) x[e] += beta * to_f(cp[rowo + n + e]);
-              if (relu) x[e] = fmaxf(x[e], 0.f);
-              if (auxp && !(to_f(auxp[rowa + n + e]) > 0.f)) x[e] = 0.f;
-            }
+            if (beta != 0.f) x[e] += beta * cin[j][e];
+            if (relu) x[e] = fmaxf(x[e], 0.f);
+            if (auxp && !(ain[j][e] > 0.f)) x[e] = 0.f;
           }
         } else if (relu) {
 #pragma unroll
@@ -551,15 +580,23 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
     }
     const int64_t co = cbase + (int64_t)m * p.ldc + n;
     const O* auxp = (const O*)p.aux;
+    float cin[W], ain[W];
+    if constexpr (V4) {
+      if (p.beta != 0.f) load4_guard(cp + co, 0, 4, true, cin);
+      if (auxp) load4_guard(auxp + cbase + (int64_t)m * p.ldaux + n, 0, 4, true, ain);
+    } else {
+      if (p.beta != 0.f) cin[0] = to_f(cp[co]);
+      if (auxp) ain[0] = to_f(auxp[cbase + (int64_t)m * p.ldaux + n]);
+    }
     O out[W];
 #pragma unroll
     for (int i = 0; i < W; ++i) {
       float x = v[i] * p.alpha;
       if (p.bias_mode == 1) x += biasp[n + i];
       else if (p.bias_mode == 2) x += biasp[m];
-      if (p.beta != 0.f) x += p.beta * to_f(cp[co + i]);
+      if (p.beta != 0.f) x += p.beta * cin[i];
       if (p.relu) x = fmaxf(x, 0.f);
-      if (auxp && !(to_f(auxp[cbase + (int64_t)m * p.ldaux + n + i]) > 0.f)) x = 0.f;
+      if (auxp && !(ain[i] > 0.f)) x = 0.f;
       out[i] = from_f<O>(x);
     }
     if constexpr (V4) {

@@ -133,6 +133,68 @@ template <typename H> struct V4h {
 template <> struct V4<__bf16> : V4h<__bf16> {};
 template <> struct V4<_Float16> : V4h<_Float16> {};
 
+// Vector forward (D = 256 NV, 4-aligned rows): lane owns elements 4*(lane + 64 j) .. +3; each
+// wave normalises LNF_RPW rows, issuing all of a row's x / residual loads before its reductions.
+constexpr int LNF_RPW = 4;
+template <typename TI, typename TO, int NV>
+__global__ __launch_bounds__(RB) void ln_fwd_vec_kernel(int64_t rows, const TI* x, int64_t ldx,
+                                                        const TI* rr, int64_t ldr,
+                                                        const float* gamma, const float* beta,
+                                                        float eps, TO* y, int64_t ldy,
+                                                        float* mean, float* rstd) {
+  constexpr int D = NV * 256;
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LNF_RPW;
+  float gm[NV][4], bt[NV][4];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    V4<float>::ld(gamma + 4 * (lane + 64 * j), gm[j]);
+    V4<float>::ld(beta + 4 * (lane + 64 * j), bt[j]);
+  }
+  for (int i = 0; i < LNF_RPW; ++i) {
+    const int64_t r = r0 + i;
+    if (r >= rows) return;
+    float v[NV][4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) V4<TI>::ld(x + r * ldx + 4 * (lane + 64 * j), v[j]);
+    if (rr) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        float t[4];
+        V4<TI>::ld(rr + r * ldr + 4 * (lane + 64 * j), t);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[j][e] += t[e];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += v[j][e];
+    const float mu = wave_sum(s) * (1.f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[j][e] - mu;
+        q += d * d;
+      }
+    const float rs = rsqrtf(wave_sum(q) * (1.f / D) + eps);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mu) * rs * gm[j][e] + bt[j][e];
+      V4<TO>::st(y + r * ldy + 4 * (lane + 64 * j), o);
+    }
+    if (lane == 0) {
+      mean[r] = mu;
+      rstd[r] = rs;
+    }
+  }
+}
+
 // NV = D / 256: lane owns elements 4*(lane + 64 j) .. +3, j < NV
 template <typename TI, typename TG, typename TD, int NV>
 __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* x, int64_t ldx,
@@ -272,9 +334,15 @@ __global__ __launch_bounds__(RB) void ln_bwd_kernel(int64_t rows, int D, const T
 // groups: each thread streams ~nblk/64 float4 loads with 4 independent accumulators, then a
 // fixed-order two-level LDS reduction (deterministic).  W % 4 == 0, stride % 4 == 0.
 constexpr int SR_G = 64;
+struct OutTab { float* p[8]; };
 __global__ __launch_bounds__(RB) void slab_reduce_kernel(int nblk, int W, const float* partials,
                                                          int64_t stride, int split, float* out0,
-                                                         float* out1, int beta_acc) {
+                                                         float* out1, int beta_acc,
+                                                         OutTab tab = OutTab{}, int grouped = 0) {
+  if (grouped) {   // group g = blockIdx.y: slabs at partials + g*nblk*stride, output tab.p[g]
+    partials += (int64_t)blockIdx.y * nblk * stride;
+    out0 = out1 = tab.p[blockIdx.y];
+  }
   __shared__ float4 red[SR_G][4];
   __shared__ float4 red2[16][4];
   const int q = threadIdx.x & 3, g = threadIdx.x >> 2;
@@ -407,7 +475,10 @@ constexpr int CS_ROWS = 256;
 // row lanes over CS_ROWS rows; each thread issues CS_ROWS/32 independent 16-B loads.
 template <typename T>
 __global__ __launch_bounds__(RB) void colsum_vec_kernel(int64_t rows, int N, const T* dy,
-                                                        int64_t ld, float* partials) {
+                                                        int64_t ld, float* partials,
+                                                        int64_t sdy = 0) {
+  dy += (int64_t)blockIdx.z * sdy;                              // group g = blockIdx.z
+  partials += (int64_t)blockIdx.z * gridDim.x * N;
   constexpr int VE = 16 / sizeof(T);
   constexpr int NC = 8 * VE;                // columns per block
   __shared__ float red[32][NC + 1];
@@ -517,10 +588,25 @@ extern "C" int jmt_layernorm_fwd(int dt_in, int dt_out, int64_t rows, int D, con
   JMT_CHECK_ARG(D > 0 && D <= 2048, "jmt_layernorm_fwd: D=%d unsupported (<=2048)", D);
   JMT_CHECK_ARG(x && y && gamma && beta && mean && rstd, "jmt_layernorm_fwd: null pointer");
   hipStream_t st = as_stream(stream);
+  const uintptr_t ai = 4 * dtype_size(dt_in), ao = 4 * dtype_size(dt_out);
+  const bool vec = (D % 256 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) && (!r || ldr % 4 == 0) &&
+                   ((uintptr_t)gamma % 16 == 0) && ((uintptr_t)beta % 16 == 0) &&
+                   ((uintptr_t)x % ai == 0) && ((uintptr_t)r % ai == 0) && ((uintptr_t)y % ao == 0);
+  const unsigned vblocks = (unsigned)((rows + 4 * LNF_RPW - 1) / (4 * LNF_RPW));
+#define JMT_LNF_VEC(NV)                                                                     \
+  hipLaunchKernelGGL((ln_fwd_vec_kernel<TI, TO, NV>), dim3(vblocks), dim3(RB), 0, st, rows, \
+                     (const TI*)x, ldx, (const TI*)r, ldr, gamma, beta, eps, (TO*)y, ldy, mean, \
+                     rstd)
   JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_out, TO,
-      hipLaunchKernelGGL((ln_fwd_kernel<TI, TO>), dim3(row_blocks(rows)), dim3(RB), 0, st, rows, D,
-                         (const TI*)x, ldx, (const TI*)r, ldr, gamma, beta, eps, (TO*)y, ldy, mean,
-                         rstd)));
+      if (vec && D == 512) { JMT_LNF_VEC(2); }
+      else if (vec && D == 768) { JMT_LNF_VEC(3); }
+      else if (vec && D == 1024) { JMT_LNF_VEC(4); }
+      else {
+        hipLaunchKernelGGL((ln_fwd_kernel<TI, TO>), dim3(row_blocks(rows)), dim3(RB), 0, st, rows,
+                           D, (const TI*)x, ldx, (const TI*)r, ldr, gamma, beta, eps, (TO*)y, ldy,
+                           mean, rstd);
+      }));
+#undef JMT_LNF_VEC
   JMT_LAUNCH_CHECK("jmt_layernorm_fwd");
   return JMT_OK;
 }
@@ -542,7 +628,11 @@ extern "C" int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, 
   hipStream_t st = as_stream(stream);
   const int nblk = jmt_layernorm_bwd_blocks(rows);
   const bool vec = (D % 256 == 0) && (ldx % 4 == 0) && (lddy % 4 == 0) && (lddx % 4 == 0) &&
-                   (!r || ldr % 4 == 0) && ((uintptr_t)gamma % 16 == 0);
+                   (!r || ldr % 4 == 0) && ((uintptr_t)gamma % 16 == 0) &&
+                   ((uintptr_t)x % (4 * dtype_size(dt_in)) == 0) &&
+                   ((uintptr_t)r % (4 * dtype_size(dt_in)) == 0) &&
+                   ((uintptr_t)dy % (4 * dtype_size(dt_dy)) == 0) &&
+                   ((uintptr_t)dx % (4 * dtype_size(dt_dx)) == 0);
 #define JMT_LNB_VEC(NV)                                                                     \
   hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV>), dim3(nblk), dim3(RB), 0, st, rows, \
                      (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd, \
@@ -610,6 +700,38 @@ extern "C" int jmt_colsum(int dt, int64_t rows, int N, const void* dy, int64_t l
                            rows, N, (const T*)dy, ld, partials));
   launch_slab_reduce(nblk, N, partials, (int64_t)N, N, db, db, beta_acc, st);
   JMT_LAUNCH_CHECK("jmt_colsum");
+  return JMT_OK;
+}
+
+extern "C" int jmt_colsum_grouped(int dt, int G, int64_t rows, int N, const void* dy, int64_t ld,
+                                  int64_t sdy, float* const* db_tab, int beta_acc,
+                                  float* partials, void* stream) {
+  JMT_CHECK_ARG(G >= 1 && G <= 8 && N > 0 && db_tab && partials && dy,
+                "jmt_colsum_grouped: bad args");
+  const int ve = 16 / dtype_size(dt);
+  JMT_CHECK_ARG((N % ve == 0) && (ld % ve == 0) && (sdy % ve == 0) && ((uintptr_t)dy % 16 == 0),
+                "jmt_colsum_grouped: N, ld, sdy must be multiples of %d and dy 16-B aligned", ve);
+  OutTab tab{};
+  for (int g = 0; g < G; ++g) {
+    JMT_CHECK_ARG(db_tab[g] != nullptr, "jmt_colsum_grouped: null output %d", g);
+    tab.p[g] = db_tab[g];
+  }
+  hipStream_t st = as_stream(stream);
+  const int nblk = jmt_colsum_blocks(rows);
+  if (nblk == 0) {
+    if (!beta_acc)
+      for (int g = 0; g < G; ++g) (void)hipMemsetAsync(db_tab[g], 0, sizeof(float) * N, st);
+    return JMT_OK;
+  }
+  JMT_DISPATCH1(dt, T,
+      hipLaunchKernelGGL((colsum_vec_kernel<T>), dim3(nblk, (N + 8 * ve - 1) / (8 * ve), G),
+                         dim3(RB), 0, st, rows, N, (const T*)dy, ld, partials, sdy));
+  JMT_LAUNCH_CHECK("jmt_colsum_grouped");
+  JMT_CHECK_ARG(N % 4 == 0, "jmt_colsum_grouped: N %% 4");
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((N + 15) / 16, G), dim3(RB), 0, st, nblk, N,
+                     (const float*)partials, (int64_t)N, N, (float*)nullptr, (float*)nullptr,
+                     beta_acc, tab, 1);
+  JMT_LAUNCH_CHECK("jmt_colsum_grouped(reduce)");
   return JMT_OK;
 }
 

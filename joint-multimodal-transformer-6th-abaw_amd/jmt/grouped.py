@@ -105,6 +105,18 @@ def _bias_grad(dy2: torch.Tensor, ld: int, rows: int, n: int, b, r0: int):
         ops.colsum(dy2, ld, rows, n, gb[r0:r0 + n], beta_acc=True)
 
 
+def _bias_grad_grouped(dy_ptr: int, G: int, ld: int, sdy: int, rows: int, n: int, bs, r0: int,
+                       cd, dev):
+    """b_g.grad[r0:r0+n] += column sums of the g-th (rows x n) block at dy_ptr + g*sdy (one
+    grouped colsum launch pair; the bs must be distinct parameters)."""
+    dbs = []
+    for b in bs:
+        gb = _grad_buffer(b)
+        dbs.append(gb[r0:r0 + n] if gb is not None else
+                   torch.empty(n, dtype=torch.float32, device=dev))
+    ops.colsum_grouped(dy_ptr, _dc(cd), G, ld, sdy, rows, n, dbs, beta_acc=True, device=dev)
+
+
 def _contig(t: torch.Tensor, cd) -> torch.Tensor:
     if t.dtype != cd:
         t = ops.cast(t.contiguous(), cd)
@@ -228,15 +240,14 @@ class EncoderGroupFn(Function):
                     R * hid, cdt, cd, dev, aux=F1, ldaux=hid)
         _gemm_wgrad([dS.data_ptr()], E, R * E, [F1.data_ptr()], hid, R * hid, R, E,
                     [p[6] for p in P], 0, cd, dev)
-        for g in range(G):
-            _bias_grad(dS[g], E, R, E, P[g][7], 0)
+        _bias_grad_grouped(dS.data_ptr(), G, E, R * E, R, E, [p[7] for p in P], 0, cd, dev)
         # dH1 = dS2 + dF1 . W1  (in place on dS: beta = 1)
         _gemm_dgrad(dF1.data_ptr(), hid, R * hid, R, hid, [p[4] for p in P], 0, dS.data_ptr(),
                     E, R * E, cdt, cd, dev, beta=1.0)
         _gemm_wgrad([dF1.data_ptr()], hid, R * hid, [H1.data_ptr()], E, R * E, R, hid,
                     [p[4] for p in P], 0, cd, dev)
-        for g in range(G):
-            _bias_grad(dF1[g], hid, R, hid, P[g][5], 0)
+        _bias_grad_grouped(dF1.data_ptr(), G, hid, R * hid, R, hid, [p[5] for p in P], 0, cd,
+                           dev)
         # LN1: dS1 = d(X + A1)
         dS1 = torch.empty_like(dS)
         ln_bwd(X, A1, dS, st1, [p[8] for p in P], [p[9] for p in P], dS1)
@@ -246,8 +257,7 @@ class EncoderGroupFn(Function):
                     R * E, cdt, cd, dev)
         _gemm_wgrad([dS1.data_ptr()], E, R * E, [O.data_ptr()], E, R * E, R, E,
                     [p[2] for p in P], 0, cd, dev)
-        for g in range(G):
-            _bias_grad(dS1[g], E, R, E, P[g][3], 0)
+        _bias_grad_grouped(dS1.data_ptr(), G, E, R * E, R, E, [p[3] for p in P], 0, cd, dev)
         # attention core -> packed dQKV
         dQKV = torch.empty(G, B, T, 3 * E, dtype=cd, device=dev)
         dsf = dQKV.view(G * B, T, 3 * E).permute(1, 0, 2)
@@ -257,8 +267,8 @@ class EncoderGroupFn(Function):
                     dS1.data_ptr(), E, R * E, cdt, cd, dev, beta=1.0)
         _gemm_wgrad([dQKV.data_ptr()], 3 * E, R * 3 * E, [X.data_ptr()], E, R * E, R, 3 * E,
                     [p[0] for p in P], 0, cd, dev)
-        for g in range(G):
-            _bias_grad(dQKV[g], 3 * E, R, 3 * E, P[g][1], 0)
+        _bias_grad_grouped(dQKV.data_ptr(), G, 3 * E, R * 3 * E, R, 3 * E, [p[1] for p in P], 0,
+                           cd, dev)
         ctx.state = None
         return (dS1, None) + (None,) * len(params)
 
@@ -337,8 +347,13 @@ class CrossAttention6Fn(Function):
         for h in halves:
             _gemm_wgrad([_ptr(dO6, i * R * E) for i in h], E, 0, [O[i * B].data_ptr() for i in h],
                         E, 0, R, E, [M[pairs[i][0]][2] for i in h], 0, cd, dev)
-        for i, (m, _, _) in enumerate(pairs):
-            _bias_grad(dO6[i], E, R, E, M[m][3], 0)
+        for h in halves:
+            if _consecutive(h):
+                _bias_grad_grouped(_ptr(dO6, h[0] * R * E), len(h), E, R * E, R, E,
+                                   [M[pairs[i][0]][3] for i in h], 0, cd, dev)
+            else:
+                for i in h:
+                    _bias_grad(dO6[i], E, R, E, M[pairs[i][0]][3], 0)
         # attention core -> packed dQKV (NP, B, T, 3E)
         dQKV = torch.empty(NP, B, T, 3 * E, dtype=cd, device=dev)
         dsf = dQKV.view(NP * B, T, 3 * E).permute(1, 0, 2)
@@ -351,8 +366,13 @@ class CrossAttention6Fn(Function):
                         [Y[pairs[i][1]].data_ptr() for i in h], E, 0, R, E, ws, 0, cd, dev)
             _gemm_wgrad([_ptr(dQKV, i * R * 3 * E + E) for i in h], 3 * E, 0,
                         [Y[pairs[i][2]].data_ptr() for i in h], E, 0, R, 2 * E, ws, E, cd, dev)
-        for i, (m, _, _) in enumerate(pairs):
-            _bias_grad(dQKV[i], 3 * E, R, 3 * E, M[m][1], 0)
+        for h in halves:
+            if _consecutive(h):
+                _bias_grad_grouped(_ptr(dQKV, h[0] * R * 3 * E), len(h), 3 * E, R * 3 * E, R,
+                                   3 * E, [M[pairs[i][0]][1] for i in h], 0, cd, dev)
+            else:
+                for i in h:
+                    _bias_grad(dQKV[i], 3 * E, R, 3 * E, M[pairs[i][0]][1], 0)
         # stream gradients: every use of stream s (as a query: rows [0,E) of W_in; as a key /
         # value: rows [E,2E) and [2E,3E)) is one K-segment of ONE dgrad GEMM (K = nseg * E)
         dY = torch.zeros(S, B, T, E, dtype=cd, device=dev) if any(
@@ -376,6 +396,10 @@ class CrossAttention6Fn(Function):
                          c=[dY[s].data_ptr()], ldc=E, beta=1.0 if c0 else 0.0, device=dev)
         ctx.state = None
         return (dY, None) + (None,) * len(params)
+
+
+def _consecutive(h) -> bool:
+    return all(b == a + 1 for a, b in zip(h[:-1], h[1:]))
 
 
 def cross_attention6(Y, modules, num_heads: int, pairs=CROSS_PAIRS):

@@ -188,6 +188,17 @@ def colsum(dy, ld, rows, N, db, beta_acc=False):
     return part
 
 
+def colsum_grouped(dy_ptr: int, dtype: int, G: int, ld: int, sdy: int, rows: int, N: int,
+                   dbs, beta_acc=True, device=None):
+    """db_g (+)= column sums of the g-th (rows x N) block at dy_ptr + g*sdy, one launch pair."""
+    nblk = _lib.load().jmt_colsum_blocks(rows)
+    part = torch.empty(max(nblk, 1) * N * G, dtype=torch.float32, device=device)
+    tab = (C.c_void_p * 8)(*[d.data_ptr() for d in dbs])
+    _lib.call("jmt_colsum_grouped", dtype, G, rows, N, dy_ptr, ld, sdy, tab, int(beta_acc),
+              part.data_ptr(), stream())
+    return part
+
+
 def copy2d(src_ptr, src_dt, dst_ptr, dst_dt, rows, cols, src_rs, src_cs, dst_rs, dst_cs,
            accumulate=False):
     _lib.call("jmt_copy2d", src_dt, dst_dt, rows, cols, src_ptr, src_rs, src_cs, dst_ptr, dst_rs,

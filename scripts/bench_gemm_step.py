@@ -1,0 +1,95 @@
+"""GEMM micro-benchmark on the grouped JMT step's launch shapes (bf16), as the model issues them
+(pointer-table weights, beta=1 accumulate, ReLU-mask aux, K-concat):
+    python scripts/bench_gemm_step.py [--cfg 0 1 5] [--only substr] [--reps 30]
+Prints per shape: us/launch, TFLOP/s, algorithmic GB/s."""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "joint-multimodal-transformer-6th-abaw_amd")]
+
+import torch  # noqa: E402
+
+from jmt import _lib, ops  # noqa: E402
+from jmt._lib import BF16, F32  # noqa: E402
+
+R = 19200
+# name, M, N, K, a_kmajor, b_kmajor, batch, c_dtype, extra
+SHAPES = [
+    ("enc b3 fwd NT 512x512", R, 512, 512, True, True, 3, BF16, {}),
+    ("enc b3 qkv NT 1536x512", R, 1536, 512, True, True, 3, BF16, {}),
+    ("enc b3 dgrad NN 512x512", R, 512, 512, True, False, 3, BF16, {}),
+    ("enc b3 dgrad NN beta", R, 512, 512, True, False, 3, BF16, {"beta": 1.0}),
+    ("enc b3 dgrad NN aux", R, 512, 512, True, False, 3, BF16, {"aux": True}),
+    ("enc b3 dgrad NN K1536 beta", R, 512, 1536, True, False, 3, BF16, {"beta": 1.0}),
+    ("ca b6 dgrad NN 512x512", R, 512, 512, True, False, 6, BF16, {}),
+    ("ca b6 kv NT 1024x512", R, 1024, 512, True, True, 6, BF16, {}),
+    ("stream dgrad kcat6 NN 512x3072", R, 512, 3072, True, False, 1, BF16, {"kcat": 6}),
+    ("head dgrad b6 NN 512x1024", R, 512, 1024, True, False, 6, BF16, {"sA0": True}),
+    ("head fwd kcat6 NT 1024x3072", R, 1024, 3072, True, True, 1, BF16, {"kcat": 6}),
+    ("wgrad b3 TN 512x512xR", 512, 512, R, False, False, 3, F32, {"beta": 1.0}),
+    ("wgrad b3 TN 1536x512xR", 1536, 512, R, False, False, 3, F32, {"beta": 1.0}),
+    ("attn dKdV b384 TN 300x512x300", 300, 512, 300, False, False, 384, BF16, {}),
+]
+
+
+def run(reps, cfg):
+    lib = _lib.load()
+    lib.jmt_gemm_set_debug(cfg << 8)
+    dev = "cuda"
+    for name, M, N, K, ak, bk, batch, cdt, ex in SHAPES:
+        r8 = lambda v: -(-v // 8) * 8
+        kc = ex.get("kcat", 0)
+        lda = r8(K // kc if kc else K) if ak else r8(M)
+        ldb = r8(K // kc if kc else K) if bk else r8(N)
+        arows = (M if ak else (K // kc if kc else K))
+        brows = (N if bk else (K // kc if kc else K))
+        nseg = kc if kc else 1
+        A = [torch.randn(batch, arows * lda, device=dev).bfloat16() for _ in range(nseg)]
+        Bt = [torch.randn(batch, brows * ldb, device=dev).bfloat16() for _ in range(max(nseg, 1))]
+        c = torch.zeros(batch, M * N, device=dev, dtype=torch.float32 if cdt == F32 else torch.bfloat16)
+        aux = torch.randn(batch, M * N, device=dev).bfloat16() if ex.get("aux") else None
+        kw = dict(M=M, N=N, K=K, ab_dtype=BF16, c_dtype=cdt, lda=lda, a_kmajor=ak, ldb=ldb,
+                  b_kmajor=bk, c=[c.data_ptr()], ldc=N, batch0=batch, sC=(M * N, 0),
+                  beta=ex.get("beta", 0.0), aux=aux, ldaux=N if aux is not None else 0, device=dev)
+        if kc:
+            kw.update(a=[a.data_ptr() for a in A], a_mode=2, a_kseg=K // kc,
+                      b=[b.data_ptr() for b in Bt], b_mode=2, b_kseg=K // kc)
+        else:
+            kw.update(a=[A[0].data_ptr()], sA=(0 if ex.get("sA0") else A[0].shape[1], 0))
+            if batch > 1 and batch <= 8:   # weights as a pointer table, as the model issues them
+                kw.update(b=[Bt[0][i].data_ptr() for i in range(batch)], b_mode=1)
+            else:
+                kw.update(b=[Bt[0].data_ptr()], sB=(Bt[0].shape[1], 0))
+        for _ in range(3):
+            ws = ops.gemm(**kw)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            ws = ops.gemm(**kw)
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / reps * 1e3
+        fl = 2.0 * M * N * K * batch
+        by = (M * K + N * K) * 2 * batch + M * N * c.element_size() * batch
+        splits = ops.auto_splits(M, N, K, batch, BF16)
+        print(json.dumps({"shape": name, "cfg": cfg, "splits": splits, "us": round(us, 2),
+                          "tflops": round(fl / us / 1e6, 1), "gbs": round(by / us / 1e3, 1)}),
+              flush=True)
+        del ws
+    lib.jmt_gemm_set_debug(0)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--cfg", type=int, nargs="*", default=[0])
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    if args.only:
+        SHAPES[:] = [s for s in SHAPES if args.only in s[0]]
+    for c in args.cfg:
+        run(args.reps, c)

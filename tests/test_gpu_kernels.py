@@ -363,3 +363,38 @@ def test_fused_attention_matches_unfused_path():
     (o1, g1), (o2, g2) = outs
     assert (o1 - o2).abs().max().item() <= 1e-2 * o2.abs().max().item()
     assert (g1 - g2).abs().max().item() <= 2e-2 * g2.abs().max().item()
+
+
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_grouped_bias_table_16bit_beta_aux(splits):
+    """Grouped launch (jmt/grouped.py): per-batch weight pointers + per-batch bias table, a 16-bit
+    output with beta=1 accumulate and the ReLU-backward aux mask (vector epilogue loads)."""
+    g = torch.Generator(device=DEV).manual_seed(21)
+    G, M, N, K = 3, 301, 136, 192
+    A = torch.randn(G, M, K, device=DEV, generator=g).bfloat16()
+    Ws = [torch.randn(N, K, device=DEV, generator=g).bfloat16() for _ in range(G)]
+    bs = [torch.randn(N, device=DEV, generator=g) for _ in range(G)]
+    C0 = torch.randn(G, M, N, device=DEV, generator=g).bfloat16()
+    aux = torch.randn(G, M, N, device=DEV, generator=g).bfloat16()
+    C = C0.clone()
+    ops.gemm(M=M, N=N, K=K, ab_dtype=BF16, c_dtype=BF16, a=[A.data_ptr()], lda=K, a_kmajor=True,
+             sA=(M * K, 0), b=[w.data_ptr() for w in Ws], ldb=K, b_kmajor=True, b_mode=1,
+             c=[C.data_ptr()], ldc=N, sC=(M * N, 0), batch0=G, beta=1.0, bias_tab=bs,
+             bias_mode=1, aux=aux, ldaux=N, splits=splits, device=DEV)
+    for i in range(G):
+        base = A[i].float() @ Ws[i].float().t() + bs[i] + C0[i].float()
+        ref = torch.where(aux[i].float() > 0, base, torch.zeros_like(base))
+        err = (C[i].float() - ref).abs().max().item()
+        assert err <= 2e-2 * max(1.0, ref.abs().max().item()), (i, err)
+
+
+def test_colsum_grouped():
+    g = torch.Generator(device=DEV).manual_seed(12)
+    G, R, N = 3, 19201, 96
+    dy = torch.randn(G, R, N, device=DEV, generator=g).bfloat16()
+    dbs = [torch.full((N,), float(i), device=DEV) for i in range(G)]
+    ops.colsum_grouped(dy.data_ptr(), BF16, G, N, R * N, R, N, dbs, beta_acc=True, device=DEV)
+    torch.cuda.synchronize()
+    for i in range(G):
+        ref = i + dy[i].float().sum(0)
+        assert (dbs[i] - ref).abs().max().item() < 1e-3
