@@ -31,9 +31,9 @@
 
 namespace jmt {
 
-constexpr int AT_QT = 64;       // rows per block
+// A block is NW waves owning 16 NW rows; every block streams the whole K/V of its (n, h) through
+// LDS (attn_waves() picks NW).
 constexpr int AT_KT = 64;       // keys per tile
-constexpr int AT_NT = 256;      // threads per block
 constexpr int AT_FWD = 0, AT_DQ = 1;
 
 struct AttnParams {
@@ -59,11 +59,11 @@ template <int DH> struct AttnGeo {
 
 // stage one tile of AT_KT key rows (row r <- source row min(k0 + r, Lk - 1)): one 1-KiB
 // LDS-DMA wave-instruction per row (DH = 512)
-template <typename T, int DH>
+template <typename T, int DH, int NW>
 __device__ __forceinline__ void stage_kv(char* img, const T* base, int64_t ld, int k0, int Lk) {
   typedef AttnGeo<DH> G;
   static_assert(G::RB == 1024, "one LDS-DMA instruction per key row");
-  constexpr int NI = AT_KT / (AT_NT / 64);
+  constexpr int NI = AT_KT / NW;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r0 = w * NI;
   char* dst = img + r0 * G::PITCH;
@@ -79,14 +79,15 @@ __device__ __forceinline__ void stage_kv(char* img, const T* base, int64_t ld, i
   }
 }
 
-template <typename T, int DH, int MODE>
-__global__ __launch_bounds__(AT_NT, 1) void attn_kernel(AttnParams p) {
+template <typename T, int DH, int MODE, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_kernel(AttnParams p) {
+  constexpr int AT_QT = 16 * NW;                  // rows per block
   typedef typename Frag16<T>::t F;
   typedef typename Frag16<T>::h Hf;
   typedef AttnGeo<DH> G;
   constexpr int KS = DH / 32;                     // k-steps of the score product
   constexpr int TD = DH / 16;                     // 16-column tiles of the accumulator
-  constexpr int NI = AT_KT / (AT_NT / 64);        // LDS-DMA instructions per wave per tile
+  constexpr int NI = AT_KT / NW;                  // LDS-DMA instructions per wave per tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* img1 = smem;
   char* img2 = smem + G::IMG;
@@ -128,8 +129,8 @@ __global__ __launch_bounds__(AT_NT, 1) void attn_kernel(AttnParams p) {
     lse2 = p.lse[prow] * 1.4426950408889634f;
   }
   // tile-0 DMA is issued behind the row loads (vmcnt retires in issue order)
-  stage_kv<T, DH>(img1, s1b, p.s1_l, 0, p.Lk);
-  stage_kv<T, DH>(img2, s2b, p.s2_l, 0, p.Lk);
+  stage_kv<T, DH, NW>(img1, s1b, p.s1_l, 0, p.Lk);
+  stage_kv<T, DH, NW>(img2, s2b, p.s2_l, 0, p.Lk);
   if constexpr (MODE == AT_DQ) {
     // Delta = rowsum(dO o O) = rowsum(P o dP)
 #pragma unroll
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(AT_NT, 1) void attn_kernel(AttnParams p) {
     wait_vmcnt<0>();                              // stream-2 tile j landed
     __syncthreads();                              // ... for all waves; stream-1 image free
     if (j + 1 < nkt) {
-      stage_kv<T, DH>(img1, s1b, p.s1_l, AT_KT * (j + 1), p.Lk);
+      stage_kv<T, DH, NW>(img1, s1b, p.s1_l, AT_KT * (j + 1), p.Lk);
       if constexpr (MODE == AT_DQ) load_p(j + 1);
     }
 
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(AT_NT, 1) void attn_kernel(AttnParams p) {
     if (j + 1 < nkt) {
       wait_vmcnt<0>();                            // stream-1 tile j+1 landed
       __syncthreads();                            // ... for all waves; stream-2 image free
-      stage_kv<T, DH>(img2, s2b, p.s2_l, AT_KT * (j + 1), p.Lk);
+      stage_kv<T, DH, NW>(img2, s2b, p.s2_l, AT_KT * (j + 1), p.Lk);
     }
   }
 
@@ -296,23 +297,34 @@ __global__ __launch_bounds__(AT_NT, 1) void attn_kernel(AttnParams p) {
   }
 }
 
-template <typename T, int DH, int MODE>
-static void launch(const AttnParams& p, int N, hipStream_t st) {
+// waves per block: 4.  8-wave blocks (half the K/V staging per FLOP) measured 3-33% SLOWER at
+// T = 300 (fwd 290 vs 280 us, dQ 400 vs 352 us for the 6 cross-attention pairs at B = 64), so the
+// kernel is not K/V-load-bound there; NW stays a template parameter for other shapes.
+static int attn_waves(int) { return 4; }
+
+template <typename T, int DH, int MODE, int NW>
+static void launch_nw(const AttnParams& p, int N, hipStream_t st) {
   constexpr int LDS = 2 * AttnGeo<DH>::IMG;
-  auto fn = attn_kernel<T, DH, MODE>;
+  auto fn = attn_kernel<T, DH, MODE, NW>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  dim3 grid((unsigned)(((p.Lq + AT_QT - 1) / AT_QT) * N * p.H));
-  hipLaunchKernelGGL(fn, grid, dim3(AT_NT), (size_t)LDS, st, p);
+  dim3 grid((unsigned)(((p.Lq + 16 * NW - 1) / (16 * NW)) * N * p.H));
+  hipLaunchKernelGGL(fn, grid, dim3(64 * NW), (size_t)LDS, st, p);
+}
+
+template <typename T, int DH, int MODE>
+static void launch(const AttnParams& p, int N, hipStream_t st) {
+  (void)attn_waves(p.Lq);
+  launch_nw<T, DH, MODE, 4>(p, N, st);
 }
 
 static int check_common(const char* name, int N, int H, int Lq, int Lk, const void* const* ptrs,
                         int nptr, const int64_t* strides, int nstr) {
   JMT_CHECK_ARG(N > 0 && H > 0 && Lq > 0 && Lk > 0 &&
-                    (int64_t)N * H * ((Lq + AT_QT - 1) / AT_QT) < (1LL << 31),
+                    (int64_t)N * H * ((Lq + 63) / 64) < (1LL << 31),
                 "%s: bad sizes", name);
   for (int i = 0; i < nptr; ++i)
     JMT_CHECK_ARG(ptrs[i] != nullptr && ((uintptr_t)ptrs[i] & 15) == 0,

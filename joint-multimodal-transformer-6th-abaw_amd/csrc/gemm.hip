@@ -63,6 +63,7 @@ struct GemmParams {
   int aux_dtype;
   int tiles_m, tiles_n;
   int c_vec4;                   // C (and aux) 4-element groups aligned for 4-element stores
+  int c_vec8;                   // C rows / base 16-B aligned (16-bit C: paired 16-B stores)
   int dbg;                      // development ablations: 1 skip MFMA, 2 skip epilogue
 };
 
@@ -79,6 +80,8 @@ struct TileCfg {
 };
 using Cfg1 = TileCfg<128, 128, 2, 2, 128, 2>;
 using Cfg5 = TileCfg<256, 256, 2, 4, 128, 2>;
+// (deeper pipelines — 256x256 KB=64 with 3-4 stages, 128x128 with 3-4 stages — measured 0-40%
+// slower on every JMT shape: profiles/r01_gemm_pipeline_depth.txt)
 
 template <typename T> struct Vec { static constexpr int n = 16 / sizeof(T); };
 
@@ -267,18 +270,35 @@ template <typename T, bool AK, bool BK, class C>
 __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB, int wm, int wn,
                                              f32x4 (&acc)[C::TM][C::TN]) {
   if constexpr (sizeof(T) == 2) {
+    // software-pipelined fragment reads: the A fragment of MFMA row i+1 (and, at the last row
+    // of a k-step, the B fragments of the next k-step) are issued before the MFMAs of row i,
+    // so LDS latency hides behind TN MFMAs instead of stalling on lgkmcnt(0)
     typedef typename Frag16<T>::t F;
+    constexpr int KS = C::KB / 64;
+    F fb[2][C::TN];
+    F fa[2];
 #pragma unroll
-    for (int ks = 0; ks < C::KB / 64; ++ks) {
-      F fb[C::TN];
+    for (int j = 0; j < C::TN; ++j)
+      fb[0][j] = read_frag16<T, BK, C::KB, C::BN>(imgB, wn * C::WTN + j * 16, 0);
+    fa[0] = read_frag16<T, AK, C::KB, C::BM>(imgA, wm * C::WTM, 0);
 #pragma unroll
-      for (int j = 0; j < C::TN; ++j)
-        fb[j] = read_frag16<T, BK, C::KB, C::BN>(imgB, wn * C::WTN + j * 16, ks);
+    for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
       for (int i = 0; i < C::TM; ++i) {
-        const F fa = read_frag16<T, AK, C::KB, C::BM>(imgA, wm * C::WTM + i * 16, ks);
+        const int idx = ks * C::TM + i;
+        const int ni = (i + 1 < C::TM) ? i + 1 : 0;
+        const int nks = (i + 1 < C::TM) ? ks : ks + 1;
+        if (nks < KS) {
+          if (ni == 0) {
 #pragma unroll
-        for (int j = 0; j < C::TN; ++j) acc[i][j] = mfma16(fb[j], fa, acc[i][j]);   // C^T tile
+            for (int j = 0; j < C::TN; ++j)
+              fb[nks & 1][j] = read_frag16<T, BK, C::KB, C::BN>(imgB, wn * C::WTN + j * 16, nks);
+          }
+          fa[(idx + 1) & 1] = read_frag16<T, AK, C::KB, C::BM>(imgA, wm * C::WTM + ni * 16, nks);
+        }
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = mfma16(fb[ks & 1][j], fa[idx & 1], acc[i][j]);   // C^T tile
       }
     }
   } else {
@@ -344,100 +364,54 @@ __device__ __forceinline__ void load4_guard(const O* row, int n, int lim, bool v
 }
 
 // ------------------------------------------------------------------ main kernel
-template <typename T, typename O, bool AK, bool BK, class C>
-__global__ __launch_bounds__(C::NT, 2 * 256 / C::NT > 0 ? 2 * 256 / C::NT : 1)
-void gemm_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int BKE = C::KB / (int)sizeof(T);         // K elements per tile
-  constexpr int IA = C::BM * C::KB;                   // A image bytes
-  constexpr int VMT = (C::BM + C::BN) * C::KB / 1024 / (C::NT / 64);   // DMA instr / wave / tile
+// one unit of work: an output tile of one batch entry and one K split
+struct GemmWork {
+  int m0, n0, b, b0, b1, split, kbeg, kend;
+};
 
+template <class C>
+__device__ __forceinline__ GemmWork decode_work(const GemmParams& p, int w) {
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int nb = p.batch0 * p.batch1;
+  const int bid = w % ntile;
+  const int rest = w / ntile;
+  GemmWork r;
+  r.b = rest % nb;
+  r.split = rest / nb;
   // XCD-aware remap (bijective): consecutive logical tiles (same A row panel) on one XCD.
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int bid = blockIdx.x;
   int wg = bid;
-  if (nwg >= 16) {
-    const int q = nwg / 8, r = nwg % 8, x = bid % 8;
-    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  if (ntile >= 16) {
+    const int q = ntile / 8, rm = ntile % 8, x = bid % 8;
+    wg = (x < rm ? x * (q + 1) : rm * (q + 1) + (x - rm) * q) + bid / 8;
   }
-  const int tm = wg / p.tiles_n;
-  const int tn = wg % p.tiles_n;
-  const int b = blockIdx.y;
-  const int b0 = b / p.batch1, b1 = b % p.batch1;
-  const int split = blockIdx.z;
+  r.m0 = (wg / p.tiles_n) * C::BM;
+  r.n0 = (wg % p.tiles_n) * C::BN;
+  r.b0 = r.b / p.batch1;
+  r.b1 = r.b % p.batch1;
+  r.kbeg = r.split * p.k_per_split;
+  r.kend = min(p.K, r.kbeg + p.k_per_split);
+  return r;
+}
 
-  const int m0 = tm * C::BM, n0 = tn * C::BN;
-  const int kbeg = split * p.k_per_split;
-  const int kend = min(p.K, kbeg + p.k_per_split);
-  const int klen = max(0, kend - kbeg);
-  const int nfull = klen / BKE;
-  const bool tail = (klen % BKE) != 0;
+// LDS-DMA of K-tile kt of work item `wk` into stage `buf`
+template <typename T, bool AK, bool BK, class C>
+__device__ __forceinline__ void issue_ktile(const GemmParams& p, char* smem, const GemmWork& wk,
+                                            int kt, int buf) {
+  constexpr int BKE = C::KB / (int)sizeof(T);
+  const int k0 = wk.kbeg + kt * BKE;
+  int ka, kb;
+  const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, wk.b0, wk.b1, p.a_kseg, k0, ka);
+  const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, wk.b0, wk.b1, p.b_kseg, k0, kb);
+  char* base = smem + buf * C::STAGE;
+  glds_tile<T, AK, C::KB, C::BM, C::NT>(base, A, p.lda, p.M, wk.m0, ka);
+  glds_tile<T, BK, C::KB, C::BN, C::NT>(base + C::BM * C::KB, B, p.ldb, p.N, wk.n0, kb);
+}
 
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int wm = wid / C::WN, wn = wid % C::WN;
-
-  f32x4 acc[C::TM][C::TN];
-#pragma unroll
-  for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto issue = [&](int kt, int buf) {
-    const int k0 = kbeg + kt * BKE;
-    int ka, kb;
-    const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, b0, b1, p.a_kseg, k0, ka);
-    const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, b0, b1, p.b_kseg, k0, kb);
-    char* base = smem + buf * C::STAGE;
-    glds_tile<T, AK, C::KB, C::BM, C::NT>(base, A, p.lda, p.M, m0, ka);
-    glds_tile<T, BK, C::KB, C::BN, C::NT>(base + IA, B, p.ldb, p.N, n0, kb);
-  };
-
-  if constexpr (C::S == 2) {
-    // prefetch one tile, two barriers per tile
-    if (nfull > 0) issue(0, 0);
-    for (int kt = 0; kt < nfull; ++kt) {
-      if (kt + 1 < nfull) {
-        issue(kt + 1, (kt + 1) & 1);
-        wait_vm(VMT);                          // tile kt landed (one newer tile in flight)
-      } else {
-        wait_vm(0);
-      }
-      __builtin_amdgcn_s_barrier();            // ... for every wave of the block
-      const char* img = smem + (kt & 1) * C::STAGE;
-      if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
-      __builtin_amdgcn_s_barrier();            // buffer (kt&1) free for tile kt+2
-    }
-  } else {
-    // S-1 tiles in flight, one barrier per tile: the barrier of iteration kt also certifies that
-    // every wave finished computing tile kt-1, whose buffer receives tile kt+S-1.
-    static_assert(C::S <= 5, "wait_tiles covers up to 3 newer tiles");
-#pragma unroll
-    for (int i = 0; i < C::S - 1; ++i)
-      if (i < nfull) issue(i, i);
-    for (int kt = 0; kt < nfull; ++kt) {
-      wait_tiles<VMT>(min(C::S - 2, nfull - 1 - kt));
-      __builtin_amdgcn_s_barrier();
-      if (kt + C::S - 1 < nfull) issue(kt + C::S - 1, (kt + C::S - 1) % C::S);
-      const char* img = smem + (kt % C::S) * C::STAGE;
-      if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
-    }
-  }
-  if (tail) {   // trailing partial K-tile: masked register staging
-    const int k0 = kbeg + nfull * BKE;
-    int ka, kb;
-    const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, b0, b1, p.a_kseg, k0, ka);
-    const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, b0, b1, p.b_kseg, k0, kb);
-    const int ka_lim = (p.a_mode == 2) ? min(p.a_kseg, ka + (kend - k0)) : kend;
-    const int kb_lim = (p.b_mode == 2) ? min(p.b_kseg, kb + (kend - k0)) : kend;
-    char* base = smem + (nfull % C::S) * C::STAGE;
-    stage_tile<T, AK, C::KB, C::BM, C::NT>(base, A, p.lda, p.M, m0, ka_lim, ka);
-    stage_tile<T, BK, C::KB, C::BN, C::NT>(base + IA, B, p.ldb, p.N, n0, kb_lim, kb);
-    __syncthreads();
-    if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(base, base + IA, wm, wn, acc);
-  }
-  __syncthreads();
-
+template <typename T, typename O, class C>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const GemmWork& wk,
+                                              f32x4 (&acc)[C::TM][C::TN], int lane, int wm,
+                                              int wn) {
+  const int m0 = wk.m0, n0 = wk.n0, b = wk.b, b0 = wk.b0, b1 = wk.b1, split = wk.split;
   // ---- epilogue.  acc[i][j] holds the TRANSPOSED 16x16 tile (the MFMA was fed B as its first
   //      operand): lane owns C row (lane&15) and the 4 consecutive columns 4*(lane>>4) + r.
   const bool partial = p.splits > 1;
@@ -470,6 +444,76 @@ void gemm_kernel(GemmParams p) {
       for (int j = 0; j < C::TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
     if (sum == 12345.678f) ((float*)cp)[0] = sum;   // keep acc live
     return;
+  }
+  if constexpr (sizeof(O) == 2 && C::TN % 2 == 0) {
+    // 16-bit C, whole wave tile in range (wave-uniform): pair the accumulators of sub-tiles j and
+    // j+1 with v_permlane16_swap so that every lane holds 8 consecutive columns of one row ->
+    // one 16-B store per lane per tile pair (half the store instructions of the 8-B path; the
+    // epilogue is store-issue-bound)
+    const int g = lane >> 4, rl = lane & 15;
+    if (!partial && p.c_vec8 && m0 + wm * C::WTM + C::WTM <= p.M &&
+        n0 + wn * C::WTN + C::WTN <= p.N) {
+      const bool plain = beta == 0.f && auxp == nullptr;
+      float bias4[C::TN][4];
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) {
+        const int n = n0 + wn * C::WTN + 16 * j + 4 * g;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bias4[j][e] = (bias_mode == 1) ? biasp[n + e] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) {
+        const int m = m0 + wm * C::WTM + 16 * i + rl;
+        const float bm = (bias_mode == 2) ? biasp[m] : 0.f;
+        const int64_t rowo = cbase + (int64_t)m * ldc;
+        const int64_t rowa = cbase + (int64_t)m * p.ldaux;
+        float cin[C::TN][4], ain[C::TN][4];
+        if (beta != 0.f) {
+#pragma unroll
+          for (int j = 0; j < C::TN; ++j)
+            load4_guard(cp + rowo, n0 + wn * C::WTN + 16 * j + 4 * g, p.N, true, cin[j]);
+        }
+        if (auxp) {
+#pragma unroll
+          for (int j = 0; j < C::TN; ++j)
+            load4_guard(auxp + rowa, n0 + wn * C::WTN + 16 * j + 4 * g, p.N, true, ain[j]);
+        }
+#pragma unroll
+        for (int jp = 0; jp < C::TN / 2; ++jp) {
+          uint32_t pk[2][2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = 2 * jp + h;
+            float x[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              x[e] = acc[i][j][e] * alpha + bias4[j][e] + bm;
+              if (!plain) {
+                if (beta != 0.f) x[e] += beta * cin[j][e];
+                if (relu) x[e] = fmaxf(x[e], 0.f);
+                if (auxp && !(ain[j][e] > 0.f)) x[e] = 0.f;
+              } else if (relu) {
+                x[e] = fmaxf(x[e], 0.f);
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              O hh[2] = {from_f<O>(x[2 * q]), from_f<O>(x[2 * q + 1])};
+              pk[h][q] = *(const uint32_t*)hh;
+            }
+          }
+          const auto r0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+          const auto r1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+          const int n = n0 + wn * C::WTN + 16 * (2 * jp + (g & 1)) + 8 * (g >> 1);
+          typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
+          // streaming (nontemporal) stores: measured 5-12% faster on the JMT shapes
+          if (p.dbg & 4) *(u32x4*)(cp + rowo + n) = v;
+          else __builtin_nontemporal_store(v, (u32x4*)(cp + rowo + n));
+        }
+      }
+      return;
+    }
   }
   {
     // direct epilogue: 4 consecutive columns per lane -> one 8-B (16-bit) / 16-B (fp32) store,
@@ -539,6 +583,84 @@ void gemm_kernel(GemmParams p) {
       }
     }
   }
+}
+
+// One block per output tile (blockIdx.x, XCD-remapped), batch entry (blockIdx.y) and K split
+// (blockIdx.z).  (A persistent form — blocks capped at the resident slots, the next tile's first
+// K-tile prefetched under the epilogue — measured 3-5% slower: profiles/r01_gemm_persistent.txt.)
+template <typename T, typename O, bool AK, bool BK, class C>
+__global__ __launch_bounds__(C::NT, 2 * 256 / C::NT > 0 ? 2 * 256 / C::NT : 1)
+void gemm_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BKE = C::KB / (int)sizeof(T);         // K elements per tile
+  constexpr int IA = C::BM * C::KB;                   // A image bytes
+  constexpr int VMT = (C::BM + C::BN) * C::KB / 1024 / (C::NT / 64);   // DMA instr / wave / tile
+
+  const int ntile = p.tiles_m * p.tiles_n;
+  const GemmWork cur = decode_work<C>(
+      p, blockIdx.x + ntile * (blockIdx.y + p.batch0 * p.batch1 * blockIdx.z));
+  const int klen = max(0, cur.kend - cur.kbeg);
+  const int nfull = klen / BKE;
+  const bool tail = (klen % BKE) != 0;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+
+  f32x4 acc[C::TM][C::TN];
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if constexpr (C::S == 2) {
+    // prefetch one tile, two barriers per tile
+    if (nfull > 0) issue_ktile<T, AK, BK, C>(p, smem, cur, 0, 0);
+    for (int kt = 0; kt < nfull; ++kt) {
+      if (kt + 1 < nfull) {
+        issue_ktile<T, AK, BK, C>(p, smem, cur, kt + 1, (kt + 1) & 1);
+        wait_vm(VMT);                          // tile kt landed (one newer tile in flight)
+      } else {
+        wait_vm(0);
+      }
+      __builtin_amdgcn_s_barrier();            // ... for every wave of the block
+      const char* img = smem + (kt & 1) * C::STAGE;
+      if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
+      __builtin_amdgcn_s_barrier();            // buffer (kt&1) free for tile kt+2
+    }
+  } else {
+    // S-1 tiles in flight, one barrier per tile: the barrier of iteration kt also certifies that
+    // every wave finished computing tile kt-1, whose buffer receives tile kt+S-1.
+    static_assert(C::S <= 5, "wait_tiles covers up to 3 newer tiles");
+#pragma unroll
+    for (int i = 0; i < C::S - 1; ++i)
+      if (i < nfull) issue_ktile<T, AK, BK, C>(p, smem, cur, i, i);
+    for (int kt = 0; kt < nfull; ++kt) {
+      wait_tiles<VMT>(min(C::S - 2, nfull - 1 - kt));
+      __builtin_amdgcn_s_barrier();
+      if (kt + C::S - 1 < nfull)
+        issue_ktile<T, AK, BK, C>(p, smem, cur, kt + C::S - 1, (kt + C::S - 1) % C::S);
+      const char* img = smem + (kt % C::S) * C::STAGE;
+      if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
+    }
+  }
+  if (tail) {   // trailing partial K-tile: masked register staging
+    const int k0 = cur.kbeg + nfull * BKE;
+    int ka, kb;
+    const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, cur.b0, cur.b1, p.a_kseg, k0,
+                                 ka);
+    const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, cur.b0, cur.b1, p.b_kseg, k0,
+                                 kb);
+    const int ka_lim = (p.a_mode == 2) ? min(p.a_kseg, ka + (cur.kend - k0)) : cur.kend;
+    const int kb_lim = (p.b_mode == 2) ? min(p.b_kseg, kb + (cur.kend - k0)) : cur.kend;
+    char* base = smem + (nfull % C::S) * C::STAGE;
+    stage_tile<T, AK, C::KB, C::BM, C::NT>(base, A, p.lda, p.M, cur.m0, ka_lim, ka);
+    stage_tile<T, BK, C::KB, C::BN, C::NT>(base + IA, B, p.ldb, p.N, cur.n0, kb_lim, kb);
+    __syncthreads();
+    if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(base, base + IA, wm, wn, acc);
+  }
+  __syncthreads();
+  gemm_epilogue<T, O, C>(p, cur, acc, lane, wm, wn);
 }
 
 // split-K reduction + epilogue.  Vector form (N % 4 == 0, C 4-element aligned): one thread per 4
@@ -784,6 +906,9 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
     for (int i = 0; i < d->n_c; ++i) cv4 = cv4 && (((uintptr_t)d->c[i] & (4 * ces - 1)) == 0);
     if (d->aux) cv4 = cv4 && (((uintptr_t)d->aux & (4 * ces - 1)) == 0) && d->ldaux % 4 == 0;
     p.c_vec4 = cv4 ? 1 : 0;
+    bool cv8 = cv4 && d->ldc % 8 == 0 && d->sC0 % 8 == 0 && d->sC1 % 8 == 0;
+    for (int i = 0; i < d->n_c; ++i) cv8 = cv8 && (((uintptr_t)d->c[i] & 15) == 0);
+    p.c_vec8 = cv8 ? 1 : 0;
   }
 
   int splits = d->splits < 1 ? 1 : d->splits;

@@ -35,9 +35,9 @@ SHAPES = [
 ]
 
 
-def run(reps, cfg):
+def run(reps, cfg, dbg=0):
     lib = _lib.load()
-    lib.jmt_gemm_set_debug(cfg << 8)
+    lib.jmt_gemm_set_debug(dbg | (cfg << 8))
     dev = "cuda"
     for name, M, N, K, ak, bk, batch, cdt, ex in SHAPES:
         r8 = lambda v: -(-v // 8) * 8
@@ -76,7 +76,7 @@ def run(reps, cfg):
         fl = 2.0 * M * N * K * batch
         by = (M * K + N * K) * 2 * batch + M * N * c.element_size() * batch
         splits = ops.auto_splits(M, N, K, batch, BF16)
-        print(json.dumps({"shape": name, "cfg": cfg, "splits": splits, "us": round(us, 2),
+        print(json.dumps({"shape": name, "cfg": cfg, "dbg": dbg, "splits": splits, "us": round(us, 2),
                           "tflops": round(fl / us / 1e6, 1), "gbs": round(by / us / 1e3, 1)}),
               flush=True)
         del ws
@@ -88,8 +88,10 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--cfg", type=int, nargs="*", default=[0])
     ap.add_argument("--only", default="")
+    ap.add_argument("--dbg", type=int, nargs="*", default=[0])
     args = ap.parse_args()
     if args.only:
         SHAPES[:] = [s for s in SHAPES if args.only in s[0]]
     for c in args.cfg:
-        run(args.reps, c)
+        for d in args.dbg:
+            run(args.reps, c, d)
