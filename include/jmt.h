@@ -198,6 +198,25 @@ int jmt_sgd_step(int64_t n, float* param, const float* grad, float* momentum_buf
                  float momentum, float dampening, float weight_decay, int nesterov,
                  int first_step, float grad_scale, void* shadow, int shadow_dt, void* stream);
 
+/* ------------------------------------------------------------------ validation post-processing
+ * val.py:313-382 + EvaluationMetrics/cccmetric.py:4-21 on the GPU.
+ * Per-video float64 arrays live in one flat buffer; video v occupies [off[v], off[v]+seglen[v]).
+ * jmt_vp_scatter: element i (frame id fid[i], the entry's own vid_length len[i], video vid[i],
+ *   predictions pv/pa, labels lv/la) is written to slot off[v] + fid - 1 (Python negative-index
+ *   rule) unless a label equals `ignore` or fid > len; among hits of one slot the element with the
+ *   largest sequence number seq0 + i wins (the reference loop's last write).  winner: one uint64
+ *   per slot, zero-initialised once; seq0 must grow across calls (seq0 += n).
+ * jmt_vp_smooth: y = uniform_filter1d(clip(x, -1, 1), size, mode='constant') per video.
+ * jmt_vp_ccc: out2[0] = ccc(x0, y0), out2[1] = ccc(x1, y1) (population std, float64). */
+int jmt_vp_scatter(int64_t n, const int* fid, const int* len, const int* vid, const int64_t* off,
+                   const int* seglen, const float* pv, const float* pa, const float* lv,
+                   const float* la, float ignore, int64_t seq0, uint64_t* winner, double* pred_v,
+                   double* pred_a, double* lab_v, double* lab_a, void* stream);
+int jmt_vp_smooth(int64_t total, int nseg, const int64_t* off, const int* seglen, const double* x,
+                  int size, double* y, void* stream);
+int jmt_vp_ccc(int64_t n, const double* x0, const double* y0, const double* x1, const double* y1,
+               double* out2, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

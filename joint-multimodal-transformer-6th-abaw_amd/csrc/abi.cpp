@@ -22,4 +22,4 @@ int set_error(int code, const char* fmt, ...) {
 extern "C" int jmt_abi_version(void) { return JMT_ABI_VERSION; }
 extern "C" const char* jmt_last_error(void) { return jmt::g_err; }
 // GEMM (3 dtypes x 4 layouts + split-K reduce) + row ops + CCC + SGD; informational only.
-extern "C" int jmt_kernel_count(void) { return 12 + 1 + 8 + 4 + 2; }
+extern "C" int jmt_kernel_count(void) { return 12 + 1 + 8 + 4 + 2 + 4; }
