@@ -36,14 +36,41 @@ PEAK_HBM_GBS = 8000.0
 D_A, D_V, E = 1024, 2048, 512
 
 
-def step_flops(B: int, T: int) -> float:
-    """Algorithmic matmul FLOPs of one training step (SURVEY.md §8d closed form, TRANSFORMER/FC,
-    L=1, h=d, plus the FcLayer): W = 3F - 2*T*d*(D_a+D_v) per window."""
+# workloads (BASELINE.json configs): the metric is quoted on c3; the others are parity /
+# profiling cases (`--config`)
+CONFIGS = {
+    "c3": dict(B=64, T=300, Da=1024, Dv=2048, fc=True, jm="TRANSFORMER", fmt="FC", dtype="bf16",
+               desc="configs[2]: FcLayer(1024,512) + Two_transformers(TRANSFORMER,FC,H=1,L=1,"
+                    "vision_in_ft=2048) + 2x CCCLoss + SGD-nesterov"),
+    "c3sa": dict(B=64, T=300, Da=1024, Dv=2048, fc=True, jm="TRANSFORMER", fmt="SELF_ATTEN",
+                 dtype="bf16", desc="configs[2] with output_format=SELF_ATTEN"),
+    "c2": dict(B=32, T=300, Da=1024, Dv=2048, fc=True, jm="NONE", fmt="FC", dtype="bf16",
+               desc="configs[1]: FcLayer(1024,512) + Two_transformers(NONE,FC) (mm_transformers)"),
+    "c4": dict(B=16, T=1024, Da=1024, Dv=2048, fc=True, jm="TRANSFORMER", fmt="FC", dtype="bf16",
+               desc="configs[3]: long window T=1024, TRANSFORMER/FC"),
+    "c5": dict(B=128, T=300, Da=1024, Dv=2048, fc=True, jm="TRANSFORMER", fmt="FC", dtype="fp16",
+               desc="configs[4]: B=128 fp16 TRANSFORMER/FC"),
+    "realdata": dict(B=64, T=16, Da=512, Dv=512, fc=False, jm="TRANSFORMER", fmt="FC",
+                     dtype="bf16", desc="shipped config_file.json: T=16 clips (512/32), R2D1 + "
+                                        "ResNet18 features (512), Two_transformers(TRANSFORMER,"
+                                        "FC,vision_in_ft=512)"),
+}
+
+
+def step_flops(B: int, T: int, Da: int = D_A, Dv: int = D_V, fc: bool = True,
+               jm: str = "TRANSFORMER", fmt: str = "FC"):
+    """Algorithmic matmul FLOPs of one training step (SURVEY.md §8d closed form for
+    TRANSFORMER/FC, L=1, h=d): F per window = input projections + out_layer_pv + 3 encoders +
+    6 cross-attentions + out_layer1 + regressors; W = 3F minus the input gradients of the
+    projections that act on leaf inputs.  None for the other heads."""
+    if jm != "TRANSFORMER" or fmt != "FC":
+        return None
     d = E
-    F = (2 * T * d * (D_A + D_V) + 4 * T * d * d + 3 * (12 * T * d * d + 4 * T * T * d)
+    proj = (2 * T * d * Da if fc else 0) + (2 * T * d * Dv if Dv != 512 else 0)
+    F = (proj + 4 * T * d * d + 3 * (12 * T * d * d + 4 * T * T * d)
          + 6 * (8 * T * d * d + 4 * T * T * d) + 24 * T * d * d + 4 * T * 1024 * 128 + 4 * T * 128)
-    W = 3 * F - 2 * T * d * (D_A + D_V)
-    return W * B
+    leaf = proj if proj else 4 * T * d * d + 2 * 6 * T * d * d
+    return (3 * F - leaf) * B
 
 
 class GemmProbe:
@@ -108,9 +135,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="windows per GPU")
-    ap.add_argument("--seq", type=int, default=300)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
+                    help="workload (c3 = the one BASELINE.json's metric is quoted on)")
+    ap.add_argument("--batch", type=int, default=None, help="windows per GPU (config default)")
+    ap.add_argument("--seq", type=int, default=None, help="T (config default)")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=64)
     ap.add_argument("--no-probe", action="store_true", help="no per-launch events (profiling)")
@@ -139,36 +168,42 @@ def main():
     from models.fc_layer import FcLayer
     from losses.loss import CCCLoss
 
+    cfg = CONFIGS[args.config]
+    args.dtype = args.dtype or cfg["dtype"]
     cd = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
-    B, T = args.batch, args.seq
+    B = args.batch or cfg["B"]
+    T = args.seq or cfg["T"]
+    Da, Dv = cfg["Da"], cfg["Dv"]
+    fl_kw = dict(Da=Da, Dv=Dv, fc=cfg["fc"], jm=cfg["jm"], fmt=cfg["fmt"])
     torch.manual_seed(0)
-    model = Two_transformers(0.0, 0.0, 1, 1, "TRANSFORMER", "FC", D_V).to(dev)
-    fc = FcLayer(D_A, E).to(dev)
+    model = Two_transformers(0.0, 0.0, 1, 1, cfg["jm"], cfg["fmt"], Dv).to(dev)
+    fc = FcLayer(Da, E).to(dev) if cfg["fc"] else None
     model_sd0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()} \
         if rank == 0 else None
     fc_sd0 = {k: v.detach().cpu().clone() for k, v in fc.state_dict().items()} \
-        if rank == 0 else None
+        if rank == 0 and fc is not None else None
     if world > 1:
         jdist.set_loss_group(dist.group.WORLD)
 
     # synthetic inputs resident in HBM, disjoint per rank (global batch = world * B)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    audio = torch.randn(B, T, D_A, device=dev, generator=g)
-    video = torch.randn(B, T, D_V, device=dev, generator=g)
+    audio = torch.randn(B, T, Da, device=dev, generator=g)
+    video = torch.randn(B, T, Dv, device=dev, generator=g)
     lv = (torch.rand(B, T, device=dev, generator=g) * 2 - 1).view(-1, B * T)
     la = (torch.rand(B, T, device=dev, generator=g) * 2 - 1).view(-1, B * T)
     crit = CCCLoss(1)
 
     def fwd_bwd():
         with JF.compute_mode(cd):
-            vo, ao = model(fc(audio), video)
+            vo, ao = model(fc(audio) if fc is not None else audio, video)
             l1 = crit(vo.view(-1, vo.shape[0] * vo.shape[1]), lv)
             l2 = crit(ao.view(-1, ao.shape[0] * ao.shape[1]), la)
             loss = l1 + l2
             loss.backward()
         return loss
 
-    params = used_parameters(fwd_bwd, list(model.parameters()) + list(fc.parameters()))
+    params = used_parameters(fwd_bwd, list(model.parameters()) +
+                             (list(fc.parameters()) if fc is not None else []))
     opt = FusedSGD(params, lr=1e-4, momentum=0.9, dampening=0.0, weight_decay=1e-4,
                    nesterov=True, shadow_dtype=cd if cd != torch.float32 else None)
 
@@ -247,10 +282,16 @@ def main():
                     "timed_over": ("eager probe steps after the timed region" if use_graph else "the timed region"),
                     "avg_launch_us": round(psum["avg_ms"] * 1e3, 2),
                     "avg_gflop_per_launch": round(psum["avg_flops"] / 1e9, 3)}
-    step_tf = step_flops(B, T) * world / (elapsed / args.steps) / 1e12
+    sfl = step_flops(B, T, **fl_kw)
+    step_mfma = None
+    if sfl is not None:
+        step_tf = sfl * world / (elapsed / args.steps) / 1e12
+        step_mfma = {"algorithmic_tflop_per_step": round(sfl * world / 1e12, 4),
+                     "achieved_tflops": round(step_tf, 1),
+                     "frac_of_peak": round(step_tf / (PEAK_BF16_TFLOPS * world), 4)}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         cpu = cpu_baseline(model_sd0, fc_sd0, args.cpu_batch, T)
 
     if rank == 0:
@@ -261,14 +302,11 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.dtype, "data": "synthetic (N(0,1) features, U(-1,1) labels, "
                                          "random-init weights)",
-            "config": {"workload": "configs[2]: FcLayer(1024,512) + Two_transformers(TRANSFORMER,"
-                                   "FC,H=1,L=1,vision_in_ft=2048) + 2x CCCLoss + SGD-nesterov",
+            "config": {"workload": cfg["desc"], "name": args.config,
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
-                       "D_a": D_A, "D_v": D_V, "parallelism": f"dp{world}"},
+                       "D_a": Da, "D_v": Dv, "parallelism": f"dp{world}"},
             "roofline": roofline,
-            "step_mfma": {"algorithmic_tflop_per_step": round(step_flops(B, T) * world / 1e12, 4),
-                          "achieved_tflops": round(step_tf, 1),
-                          "frac_of_peak": round(step_tf / (PEAK_BF16_TFLOPS * world), 4)},
+            "step_mfma": step_mfma,
             "cpu_baseline": cpu,
             "final_loss": round(last_loss, 6),
             "graph": bool(use_graph),
