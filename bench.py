@@ -82,6 +82,7 @@ class GemmProbe:
         self.on = False
         self.events = []
         self.flops = []
+        self.bytes = []
 
     def __call__(self, info, launch):
         if not self.on or (info["ab_dtype"], info["a_kmajor"], info["b_kmajor"]) != self.key:
@@ -93,6 +94,10 @@ class GemmProbe:
         e.record()
         self.events.append((s, e))
         self.flops.append(2.0 * info["M"] * info["N"] * info["K"] * info["batch"])
+        ab = 4 if info["ab_dtype"] == 0 else 2
+        cb = 4 if info["c_dtype"] == 0 else 2
+        self.bytes.append(info["batch"] * ((info["M"] + info["N"]) * info["K"] * ab +
+                                           info["M"] * info["N"] * cb))
         return r
 
     def summary(self):
@@ -101,6 +106,7 @@ class GemmProbe:
         ms = [s.elapsed_time(e) for s, e in self.events]
         return {"launches": len(ms), "avg_ms": sum(ms) / len(ms),
                 "avg_flops": sum(self.flops) / len(self.flops),
+                "avg_bytes": sum(self.bytes) / len(self.bytes),
                 "total_ms": sum(ms)}
 
 
@@ -272,12 +278,22 @@ def main():
 
     psum = probe.summary()
     roofline = None
+    # HBM bytes per launch of the same kernel family from the committed PMC passes
+    # (scripts/pmc_bench.sh: FETCH_SIZE / WRITE_SIZE, separate rocprofv3 passes, gfx950 correction)
+    traffic, traffic_src = None, None
+    tpath = os.path.join(REPO, "profiles", "r01_pmc_bench", "traffic_nt_gemm.json")
+    if args.config == "c3" and cd == torch.bfloat16 and os.path.exists(tpath):
+        traffic = round(json.load(open(tpath))["hbm_bytes_per_launch"])
+        traffic_src = os.path.relpath(tpath, REPO)
     if psum:
         achieved = psum["avg_flops"] / (psum["avg_ms"] * 1e-3) / 1e12
         roofline = {"bound": "mfma", "kernel": "gemm_kernel<bf16,Kmajor,Kmajor> (NT: all forward "
                     "linears + attention scores)", "achieved": round(achieved, 1),
                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                    "traffic_unit": "HBM bytes per launch (PMC)",
+                    "traffic_source": traffic_src,
+                    "algorithmic_bytes_per_launch": round(psum["avg_bytes"]),
                     "launches_per_step": psum["launches"] // (args.probe_steps if use_graph else args.steps),
                     "timed_over": ("eager probe steps after the timed region" if use_graph else "the timed region"),
                     "avg_launch_us": round(psum["avg_ms"] * 1e3, 2),

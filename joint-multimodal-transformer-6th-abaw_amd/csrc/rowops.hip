@@ -33,6 +33,13 @@ __global__ __launch_bounds__(RB) void l2norm_fwd_kernel(int64_t rows, int D, con
   if (lane == 0) inv_norm[r] = inv;
 }
 
+// single-pass form (D = 256 NV, rows 4-aligned): the row stays in registers between the norm
+// and the scaled write, so x is read once (the loop form above reads it twice)
+template <typename TX, typename TY, int NV>
+__global__ __launch_bounds__(RB) void l2norm_fwd_vec_kernel(int64_t rows, const TX* x,
+                                                            int64_t ldx, TY* y, int64_t ldy,
+                                                            float* inv_norm, float eps);
+
 template <typename TX, typename TG, typename TD>
 __global__ __launch_bounds__(RB) void l2norm_bwd_kernel(int64_t rows, int D, const TX* x,
                                                         int64_t ldx, const TG* dy, int64_t lddy,
@@ -106,7 +113,7 @@ __global__ __launch_bounds__(RB) void ln_fwd_kernel(int64_t rows, int D, const T
   }
 }
 
-constexpr int LN_ROWS_PER_BLOCK = 32;    // 8 rows per wave (600 blocks at B*T = 19200)
+constexpr int LN_ROWS_PER_BLOCK = 16;    // 4 rows per wave (1200 blocks at B*T = 19200)
 
 // 4-element vector loads/stores (8 B for 16-bit types, 16 B for f32); rows are 4-aligned
 template <typename T> struct V4;
@@ -132,6 +139,33 @@ template <typename H> struct V4h {
 };
 template <> struct V4<__bf16> : V4h<__bf16> {};
 template <> struct V4<_Float16> : V4h<_Float16> {};
+
+template <typename TX, typename TY, int NV>
+__global__ __launch_bounds__(RB) void l2norm_fwd_vec_kernel(int64_t rows, const TX* x,
+                                                            int64_t ldx, TY* y, int64_t ldy,
+                                                            float* inv_norm, float eps) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  float v[NV][4];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) V4<TX>::ld(x + r * ldx + 4 * (lane + 64 * j), v[j]);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += v[j][e] * v[j][e];
+  s = wave_sum(s);
+  const float inv = 1.f / fmaxf(sqrtf(s), eps);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = v[j][e] * inv;
+    V4<TY>::st(y + r * ldy + 4 * (lane + 64 * j), o);
+  }
+  if (lane == 0) inv_norm[r] = inv;
+}
 
 // Vector forward (D = 256 NV, 4-aligned rows): lane owns elements 4*(lane + 64 j) .. +3; each
 // wave normalises LNF_RPW rows, issuing all of a row's x / residual loads before its reductions.
@@ -525,6 +559,41 @@ __global__ __launch_bounds__(RB) void colsum_kernel(int64_t rows, int N, const T
 }
 
 // ------------------------------------------------------------------ strided copy
+// Row-contiguous copy / cast (both column strides 1, cols % 8 == 0, 16-B aligned rows when the
+// element is 16-bit; 8 elements per thread per step: 16-B loads of 16-bit, 2x16-B of f32).
+template <typename TS, typename TD>
+__global__ __launch_bounds__(RB) void copy_rows_vec_kernel(int64_t rows, int64_t cols,
+                                                           const TS* src, int64_t srs, TD* dst,
+                                                           int64_t drs) {
+  const int64_t c8 = cols / 8;
+  const int64_t total = rows * c8;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / c8, c = (e - r * c8) * 8;
+    const TS* sp = src + r * srs + c;
+    TD* dp = dst + r * drs + c;
+    float v[8];
+    if constexpr (sizeof(TS) == 4) {
+      const float4 a = *(const float4*)sp, b = *(const float4*)(sp + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+      const uint4 u = *(const uint4*)sp;
+      const TS* h = (const TS*)&u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = to_f(h[i]);
+    }
+    if constexpr (sizeof(TD) == 4) {
+      *(float4*)dp = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(dp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      TD h[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) h[i] = from_f<TD>(v[i]);
+      *(uint4*)dp = *(const uint4*)h;
+    }
+  }
+}
+
 __global__ __launch_bounds__(RB) void copy2d_kernel(int sdt, int ddt, int64_t rows, int64_t cols,
                                                     const void* src, int64_t srs, int64_t scs,
                                                     void* dst, int64_t drs, int64_t dcs, int acc) {
@@ -559,9 +628,21 @@ extern "C" int jmt_l2norm_fwd(int x_dt, int y_dt, int64_t rows, int D, const voi
   if (rows == 0) return JMT_OK;
   JMT_CHECK_ARG(D > 0 && x && y && inv_norm, "jmt_l2norm_fwd: bad args");
   hipStream_t st = as_stream(stream);
+  const bool vec = (D == 512 || D == 1024 || D == 2048) && ldx % 4 == 0 && ldy % 4 == 0 &&
+                   ((uintptr_t)x % (4 * dtype_size(x_dt))) == 0 &&
+                   ((uintptr_t)y % (4 * dtype_size(y_dt))) == 0;
+#define JMT_L2V(NV)                                                                          \
+  hipLaunchKernelGGL((l2norm_fwd_vec_kernel<TX, TY, NV>), dim3(row_blocks(rows)), dim3(RB), 0, \
+                     st, rows, (const TX*)x, ldx, (TY*)y, ldy, inv_norm, eps)
   JMT_DISPATCH1(x_dt, TX, JMT_DISPATCH1(y_dt, TY,
-      hipLaunchKernelGGL((l2norm_fwd_kernel<TX, TY>), dim3(row_blocks(rows)), dim3(RB), 0, st,
-                         rows, D, (const TX*)x, ldx, (TY*)y, ldy, inv_norm, eps)));
+      if (vec && D == 512) { JMT_L2V(2); }
+      else if (vec && D == 1024) { JMT_L2V(4); }
+      else if (vec && D == 2048) { JMT_L2V(8); }
+      else {
+        hipLaunchKernelGGL((l2norm_fwd_kernel<TX, TY>), dim3(row_blocks(rows)), dim3(RB), 0, st,
+                           rows, D, (const TX*)x, ldx, (TY*)y, ldy, inv_norm, eps);
+      }));
+#undef JMT_L2V
   JMT_LAUNCH_CHECK("jmt_l2norm_fwd");
   return JMT_OK;
 }
@@ -742,6 +823,19 @@ extern "C" int jmt_copy2d(int src_dt, int dst_dt, int64_t rows, int64_t cols, co
   JMT_CHECK_ARG(src && dst, "jmt_copy2d: null pointer");
   JMT_CHECK_ARG(src_dt >= 0 && src_dt <= 2 && dst_dt >= 0 && dst_dt <= 2, "jmt_copy2d: dtype");
   const int64_t total = rows * cols;
+  const bool vec = !accumulate && src_cs == 1 && dst_cs == 1 && cols % 8 == 0 &&
+                   src_rs % 8 == 0 && dst_rs % 8 == 0 && ((uintptr_t)src % 16) == 0 &&
+                   ((uintptr_t)dst % 16) == 0;
+  if (vec) {
+    int64_t vb = (total / 8 + RB - 1) / RB;
+    const unsigned blocks = (unsigned)(vb > 16384 ? 16384 : (vb < 1 ? 1 : vb));
+    JMT_DISPATCH1(src_dt, TS, JMT_DISPATCH1(dst_dt, TD,
+        hipLaunchKernelGGL((copy_rows_vec_kernel<TS, TD>), dim3(blocks), dim3(RB), 0,
+                           as_stream(stream), rows, cols, (const TS*)src, src_rs, (TD*)dst,
+                           dst_rs)));
+    JMT_LAUNCH_CHECK("jmt_copy2d(vec)");
+    return JMT_OK;
+  }
   int blocks = (int)((total + RB - 1) / RB);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(copy2d_kernel, dim3(blocks), dim3(RB), 0, as_stream(stream), src_dt, dst_dt,

@@ -101,7 +101,7 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
         d.ws_bytes = nbytes
     launch = lambda: _lib.check(_lib.load().jmt_gemm(C.byref(d), stream()), "jmt_gemm")
     if _launch_hook is not None:
-        _launch_hook({"ab_dtype": ab_dtype, "a_kmajor": bool(a_kmajor),
+        _launch_hook({"ab_dtype": ab_dtype, "c_dtype": c_dtype, "a_kmajor": bool(a_kmajor),
                       "b_kmajor": bool(b_kmajor), "M": M, "N": N, "K": K,
                       "batch": batch0 * batch1}, launch)
     else:
