@@ -171,13 +171,20 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_kernel(AttnParams p) {
     f32x4 s[4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    {   // score fragments double-buffered: k-step ks+1's reads issue before k-step ks's MFMAs
+      F kf[2][4];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      F kf[4];
+      for (int kt = 0; kt < 4; ++kt) kf[0][kt] = *(const F*)(s1l + kt * 16 * G::PITCH);
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) kf[kt] = *(const F*)(s1l + kt * 16 * G::PITCH + ks * 64);
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) {
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) s[kt] = mfma16(kf[kt], qf[ks], s[kt]);
+          for (int kt = 0; kt < 4; ++kt)
+            kf[(ks + 1) & 1][kt] = *(const F*)(s1l + kt * 16 * G::PITCH + (ks + 1) * 64);
+        }
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) s[kt] = mfma16(kf[ks & 1][kt], qf[ks], s[kt]);
+      }
     }
     const int kbase = AT_KT * j + 4 * g;
     F pf[2];
@@ -256,16 +263,24 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_kernel(AttnParams p) {
     }
 
     // ---- accumulate: acc[t] += sum_k pf(k) * stream2[k][16t + 4g + r]
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int t = 0; t < TD; ++t) {
+    // fragment reads run PD MFMAs ahead (a ring of PD fragments): the transposed LDS reads of
+    // fragment q+PD are in flight while MFMA q executes, instead of one read->wait->MFMA chain
+    {
+      constexpr int NQ = 2 * TD, PD = 4;
+      auto vread = [&](int q) -> F {
+        const int u = q / TD, t = q % TD;
         const Hf lo = tr_read<Hf>(s2l + 32 * u * G::PITCH + 32 * t);
         const Hf hi = tr_read<Hf>(s2l + (32 * u + 16) * G::PITCH + 32 * t);
-        F vf;
-        vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
-        vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
-        o[t] = mfma16(vf, pf[u], o[t]);
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      };
+      F ring[PD];
+#pragma unroll
+      for (int q = 0; q < PD; ++q) ring[q] = vread(q);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const F vf = ring[q % PD];
+        if (q + PD < NQ) ring[q % PD] = vread(q + PD);
+        o[q % TD] = mfma16(vf, pf[q / TD], o[q % TD]);
       }
     }
     if (j + 1 < nkt) {
