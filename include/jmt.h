@@ -217,6 +217,14 @@ int jmt_vp_smooth(int64_t total, int nseg, const int64_t* off, const int* seglen
 int jmt_vp_ccc(int64_t n, const double* x0, const double* y0, const double* x1, const double* y1,
                double* out2, void* stream);
 
+/* ------------------------------------------------------------------ feature store gather
+ * SURVEY.md §8f row 2 (replaces the per-clip np.load + torch.cat of train.py:150-171 and the
+ * per-batch H2D copy): out[r, 0:D] = (dt_out) table[idx[r], 0:D] for r < rows, zero rows where
+ * idx[r] < 0 or >= nrows_table (left padding).  ld's multiples of 8 elements, 16-B aligned. */
+int jmt_gather_rows(int dt_table, int dt_out, int64_t rows, int D, const void* table, int64_t ldt,
+                    int64_t nrows_table, const int64_t* idx, void* out, int64_t ldo,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

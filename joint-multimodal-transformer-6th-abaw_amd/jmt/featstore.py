@@ -1,0 +1,153 @@
+"""HBM-resident feature store.
+
+The reference assembles the wavLM audio features of every training window inside the hot loop:
+for each sample and each of its clips it builds a path, `np.load`s one 768-float vector from disk
+and `torch.cat`s it onto the window (train.py:150-171, files written by
+create_wavlm_audio_feat.py:7-33 as <video>/<k>.npy).  Here the per-clip vectors of every video are
+packed once into one contiguous table per modality (`FeatureStoreWriter`), the table is loaded
+into HBM once (`FeatureStore`; a 288 GB device holds any Aff-Wild2 feature set many times over),
+and a window batch is assembled on the device by one gather launch (csrc/gather.hip): no file
+I/O, no host loop over clips and no per-batch host-to-device copy in the training step.
+
+Reference semantics kept (train.py:157-159): a clip whose .npy file does not exist re-uses the
+vector of the previously loaded clip (`feat_numpy` keeps its last value across clips AND
+samples); a missing very first clip is an error (a NameError in the reference).  Window entries
+given as None are padding rows (zeros, padSequence.py:14-21).
+
+On-disk layout (`path/`): meta.json {modalities: {name: {dim, dtype}}, videos: [{name, offset,
+length}], missing: {name: [rows]}} and one row-major <modality>.bin per modality.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .ops import dt, stream
+
+_NP = {"float32": np.float32, "float16": np.float16}
+
+
+class FeatureStoreWriter:
+    def __init__(self, path: str, modalities: Dict[str, int], dtype: str = "float16"):
+        assert dtype in _NP
+        os.makedirs(path, exist_ok=True)
+        self.path, self.dims, self.dtype = path, dict(modalities), dtype
+        self.videos: List[dict] = []
+        self.missing: Dict[str, List[int]] = {m: [] for m in modalities}
+        self.rows = 0
+        self.files = {m: open(os.path.join(path, m + ".bin"), "wb") for m in modalities}
+
+    def add_video(self, name: str, feats: Dict[str, np.ndarray],
+                  present: Optional[Dict[str, np.ndarray]] = None):
+        """feats[m]: (length, dim) rows of clip 1..length; present[m]: bool per row (False = the
+        clip's file is missing; its row content is ignored)."""
+        n = {v.shape[0] for v in feats.values()}
+        assert len(n) == 1, "all modalities need one row per clip"
+        length = n.pop()
+        for m, a in feats.items():
+            assert a.shape[1] == self.dims[m], (m, a.shape)
+            self.files[m].write(np.ascontiguousarray(a, dtype=_NP[self.dtype]).tobytes())
+            if present is not None and m in present:
+                self.missing[m] += [self.rows + i for i in np.nonzero(~present[m])[0].tolist()]
+        self.videos.append({"name": name, "offset": self.rows, "length": int(length)})
+        self.rows += int(length)
+
+    def close(self):
+        for f in self.files.values():
+            f.close()
+        meta = {"modalities": {m: {"dim": d, "dtype": self.dtype} for m, d in self.dims.items()},
+                "videos": self.videos, "rows": self.rows, "missing": self.missing}
+        with open(os.path.join(self.path, "meta.json"), "w") as f:
+            json.dump(meta, f)
+
+    @staticmethod
+    def from_npy_tree(path: str, root: str, modality: str = "wavlm", dim: int = 768,
+                      dtype: str = "float16", videos: Optional[Sequence[str]] = None,
+                      lengths: Optional[Dict[str, int]] = None):
+        """Pack create_wavlm_audio_feat.py's tree <root>/<video>/<k>.npy (k = 1..length)."""
+        w = FeatureStoreWriter(path, {modality: dim}, dtype)
+        names = sorted(os.listdir(root)) if videos is None else list(videos)
+        for v in names:
+            d = os.path.join(root, v)
+            if lengths is not None and v in lengths:
+                length = lengths[v]
+            else:
+                ks = [int(f[:-4]) for f in os.listdir(d) if f.endswith(".npy")]
+                length = max(ks) if ks else 0
+            a = np.zeros((length, dim), dtype=np.float32)
+            ok = np.zeros(length, dtype=bool)
+            for k in range(1, length + 1):
+                f = os.path.join(d, f"{k}.npy")
+                if os.path.exists(f):
+                    a[k - 1] = np.load(f)           # numeric arrays only (allow_pickle=False)
+                    ok[k - 1] = True
+            w.add_video(v, {modality: a}, {modality: ok})
+        w.close()
+        return path
+
+
+class FeatureStore:
+    def __init__(self, path: str, device=None):
+        with open(os.path.join(path, "meta.json")) as f:
+            self.meta = json.load(f)
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.rows = int(self.meta["rows"])
+        self.video_index = {v["name"]: (v["offset"], v["length"]) for v in self.meta["videos"]}
+        self.tables: Dict[str, torch.Tensor] = {}
+        self.present: Dict[str, np.ndarray] = {}
+        for m, info in self.meta["modalities"].items():
+            D = int(info["dim"])
+            ld = -(-D // 8) * 8                     # 16-B aligned rows for the gather kernel
+            host = np.fromfile(os.path.join(path, m + ".bin"), dtype=_NP[info["dtype"]])
+            host = host.reshape(self.rows, D)
+            t = torch.zeros(max(self.rows, 1), ld, dtype=torch.from_numpy(host[:0]).dtype)
+            t[:self.rows, :D] = torch.from_numpy(host)
+            self.tables[m] = t.to(self.device)     # one host->device copy, at load time
+            ok = np.ones(self.rows, dtype=bool)
+            ok[np.asarray(self.meta["missing"].get(m, []), dtype=np.int64)] = False
+            self.present[m] = ok
+
+    def dim(self, modality: str) -> int:
+        return int(self.meta["modalities"][modality]["dim"])
+
+    def window_rows(self, modality: str, clips: Sequence[Sequence[Optional[Tuple[str, int]]]],
+                    last: Optional[int] = None) -> Tuple[np.ndarray, Optional[int]]:
+        """(B, T) table rows of a batch: clips[b][t] = (video, clip number from 1) or None
+        (padding).  A missing clip re-uses the previously loaded row (train.py:157-159), carried
+        across samples and calls through `last`.  Returns (rows, new last)."""
+        pres = self.present[modality]
+        B = len(clips)
+        T = max((len(c) for c in clips), default=0)
+        out = np.full((B, T), -1, dtype=np.int64)
+        for b, row in enumerate(clips):
+            for t, c in enumerate(row):
+                if c is None:
+                    continue
+                off, length = self.video_index[c[0]]
+                k = int(c[1])
+                r = off + k - 1 if 1 <= k <= length else -1
+                if r >= 0 and pres[r]:
+                    last = r
+                elif last is None:
+                    raise KeyError(f"clip {c} has no feature file and no clip was loaded before "
+                                   "it (the reference fails here)")
+                out[b, t] = last
+        return out, last
+
+    def gather(self, modality: str, rows, out_dtype: torch.dtype = torch.float32) -> torch.Tensor:
+        """(B, T, D) features of the given table rows (-1 = zero padding row), on the device."""
+        tab = self.tables[modality]
+        D = self.dim(modality)
+        idx = torch.as_tensor(rows, dtype=torch.int64).to(self.device)
+        B, T = idx.shape
+        ld = -(-D // 8) * 8
+        out = torch.empty(B, T, ld, dtype=out_dtype, device=self.device)
+        _lib.call("jmt_gather_rows", dt(tab), dt(out_dtype), B * T, D, tab.data_ptr(),
+                  tab.shape[1], self.rows, idx.data_ptr(), out.data_ptr(), ld, stream())
+        self._keep = idx
+        return out[..., :D]
