@@ -168,7 +168,7 @@ def main():
     from jmt import functional as JF
     from jmt import ops
     from jmt import dist as jdist
-    from jmt.optim import FusedSGD, used_parameters
+    from jmt.optim import FusedSGD, GradScaler, used_parameters
     from jmt.graph import GraphedStep
     from models.two_transformers import Two_transformers
     from models.fc_layer import FcLayer
@@ -199,13 +199,17 @@ def main():
     la = (torch.rand(B, T, device=dev, generator=g) * 2 - 1).view(-1, B * T)
     crit = CCCLoss(1)
 
+    # fp16 trains under loss scaling as the reference does (train.py:89,314-316); the scaler's
+    # state lives on the device, so the step stays one graph replay
+    scaler = GradScaler(device=dev) if cd == torch.float16 else None
+
     def fwd_bwd():
         with JF.compute_mode(cd):
             vo, ao = model(fc(audio) if fc is not None else audio, video)
             l1 = crit(vo.view(-1, vo.shape[0] * vo.shape[1]), lv)
             l2 = crit(ao.view(-1, ao.shape[0] * ao.shape[1]), la)
             loss = l1 + l2
-            loss.backward()
+            (scaler.scale(loss) if scaler is not None else loss).backward()
         return loss
 
     params = used_parameters(fwd_bwd, list(model.parameters()) +
@@ -220,7 +224,11 @@ def main():
             bucket = 16 << 20   # elements per all-reduce bucket
             for off in range(0, opt.numel, bucket):
                 dist.all_reduce(opt.flat_g[off:off + bucket])
-        opt.step()
+        if scaler is not None:
+            scaler.step(opt)
+            scaler.update()
+        else:
+            opt.step()
         return loss
 
     probe = GemmProbe((ops.dt(cd), True, True))
@@ -256,7 +264,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     probe.on = False
-    last_loss = float(loss)
+    last_loss = float(loss.detach())
     if use_graph and not args.no_probe:
         # per-launch HIP events cannot sit inside the replayed graph: the dominant kernel is
         # timed over `probe_steps` eager steps right after the timed region, with the same
@@ -287,8 +295,8 @@ def main():
         traffic_src = os.path.relpath(tpath, REPO)
     if psum:
         achieved = psum["avg_flops"] / (psum["avg_ms"] * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "kernel": "gemm_kernel<bf16,Kmajor,Kmajor> (NT: all forward "
-                    "linears + attention scores)", "achieved": round(achieved, 1),
+        roofline = {"bound": "mfma", "kernel": f"gemm_kernel<{args.dtype},Kmajor,Kmajor> (NT: all "
+                    "forward linears + attention scores)", "achieved": round(achieved, 1),
                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                     "traffic_unit": "HBM bytes per launch (PMC)",
@@ -320,7 +328,8 @@ def main():
                                          "random-init weights)",
             "config": {"workload": cfg["desc"], "name": args.config,
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
-                       "D_a": Da, "D_v": Dv, "parallelism": f"dp{world}"},
+                       "D_a": Da, "D_v": Dv, "parallelism": f"dp{world}",
+                       "loss_scaling": "device GradScaler" if scaler is not None else None},
             "roofline": roofline,
             "step_mfma": step_mfma,
             "cpu_baseline": cpu,

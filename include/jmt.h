@@ -198,6 +198,19 @@ int jmt_sgd_step(int64_t n, float* param, const float* grad, float* momentum_buf
                  float momentum, float dampening, float weight_decay, int nesterov,
                  int first_step, float grad_scale, void* shadow, int shadow_dt, void* stream);
 
+/* GradScaler with device-resident state (train.py:89,314-316): amp[5] fp32 = {scale, inv_scale,
+ * found_inf, growth_tracker, steps_taken}.  jmt_amp_check sets found_inf if any grad*inv_scale is
+ * not finite; jmt_sgd_step_amp is jmt_sgd_step on the unscaled gradient, skipped when found_inf
+ * (first-step momentum rule: allow_first && steps_taken == 0); jmt_amp_update is torch's _amp_update_scale_
+ * (backoff on overflow, growth after growth_interval clean steps) and clears found_inf. */
+int jmt_amp_check(int64_t n, const float* grad, float* amp, void* stream);
+int jmt_sgd_step_amp(int64_t n, float* param, const float* grad, float* momentum_buf, float lr,
+                     float momentum, float dampening, float weight_decay, int nesterov,
+                     int allow_first, const float* amp, void* shadow, int shadow_dt,
+                     void* stream);
+int jmt_amp_update(float* amp, float growth_factor, float backoff_factor, int growth_interval,
+                   void* stream);
+
 /* ------------------------------------------------------------------ validation post-processing
  * val.py:313-382 + EvaluationMetrics/cccmetric.py:4-21 on the GPU.
  * Per-video float64 arrays live in one flat buffer; video v occupies [off[v], off[v]+seglen[v]).

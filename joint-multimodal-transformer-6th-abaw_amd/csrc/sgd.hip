@@ -54,3 +54,114 @@ extern "C" int jmt_sgd_step(int64_t n, float* param, const float* grad, float* m
   JMT_LAUNCH_CHECK("jmt_sgd_step");
   return JMT_OK;
 }
+
+// ------------------------------------------------------------------ GradScaler (train.py:89,
+// 314-316: scaler.scale(loss).backward(); scaler.step(optimizer); scaler.update()) with all state
+// on the device, so a training step with loss scaling needs no host synchronisation and captures
+// into a hipGraph.  amp[5] (fp32): scale, inv_scale, found_inf, growth_tracker, steps_taken.
+namespace jmt {
+
+__global__ __launch_bounds__(256) void amp_check_kernel(int64_t n, const float* __restrict__ g,
+                                                        float* amp) {
+  const float inv = amp[1];
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    bad |= !isfinite(g[i] * inv);
+  if (__any(bad) && (threadIdx.x & 63) == 0) amp[2] = 1.f;   // same value from every writer
+}
+
+// torch.optim.SGD step on the unscaled gradient, skipped when found_inf (torch's scaler.step
+// skips optimizer.step()); the momentum buffer's first-step rule follows the device step count.
+template <typename TS>
+__global__ __launch_bounds__(256) void sgd_amp_kernel(int64_t n, float* __restrict__ p,
+                                                      const float* __restrict__ g,
+                                                      float* __restrict__ buf, float lr, float mom,
+                                                      float damp, float wd, int nesterov,
+                                                      int allow_first, const float* amp,
+                                                      TS* __restrict__ shadow) {
+  if (amp[2] != 0.f) return;
+  const float gs = amp[1];
+  const int first = allow_first && amp[4] == 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float w = p[i];
+    float d = g[i] * gs;
+    if (wd != 0.f) d += wd * w;
+    if (mom != 0.f) {
+      float b = first ? d : buf[i] * mom + (1.f - damp) * d;
+      buf[i] = b;
+      d = nesterov ? d + mom * b : b;
+    }
+    const float nw = w - lr * d;
+    p[i] = nw;
+    if (shadow) shadow[i] = from_f<TS>(nw);
+  }
+}
+
+// torch's _amp_update_scale_: backoff on overflow, growth after growth_interval clean steps
+__global__ void amp_update_kernel(float* amp, float growth, float backoff, int interval) {
+  if (threadIdx.x != 0) return;
+  float scale = amp[0];
+  if (amp[2] != 0.f) {
+    scale *= backoff;
+    amp[3] = 0.f;
+  } else {
+    amp[4] += 1.f;
+    const float t = amp[3] + 1.f;
+    if (t >= (float)interval) {
+      const float ns = scale * growth;
+      if (isfinite(ns)) scale = ns;
+      amp[3] = 0.f;
+    } else {
+      amp[3] = t;
+    }
+  }
+  amp[0] = scale;
+  amp[1] = (float)(1.0 / (double)scale);   // unscale_: scale.double().reciprocal().float()
+  amp[2] = 0.f;
+}
+
+}  // namespace jmt
+
+extern "C" int jmt_amp_check(int64_t n, const float* grad, float* amp, void* stream) {
+  JMT_CHECK_ARG(grad && amp && n >= 0, "jmt_amp_check: bad args");
+  if (n == 0) return JMT_OK;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(amp_check_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), n, grad,
+                     amp);
+  JMT_LAUNCH_CHECK("jmt_amp_check");
+  return JMT_OK;
+}
+
+extern "C" int jmt_sgd_step_amp(int64_t n, float* param, const float* grad, float* momentum_buf,
+                                float lr, float momentum, float dampening, float weight_decay,
+                                int nesterov, int allow_first, const float* amp, void* shadow,
+                                int shadow_dt, void* stream) {
+  if (n == 0) return JMT_OK;
+  JMT_CHECK_ARG(param && grad && amp, "jmt_sgd_step_amp: null pointer");
+  JMT_CHECK_ARG(momentum == 0.f || momentum_buf, "jmt_sgd_step_amp: momentum needs a buffer");
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t st = as_stream(stream);
+  if (shadow && shadow_dt == JMT_F16)
+    hipLaunchKernelGGL((sgd_amp_kernel<_Float16>), dim3(blocks), dim3(256), 0, st, n, param, grad,
+                       momentum_buf, lr, momentum, dampening, weight_decay, nesterov, allow_first,
+                       amp, (_Float16*)shadow);
+  else
+    hipLaunchKernelGGL((sgd_amp_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, n, param, grad,
+                       momentum_buf, lr, momentum, dampening, weight_decay, nesterov, allow_first,
+                       amp, (__bf16*)shadow);
+  JMT_LAUNCH_CHECK("jmt_sgd_step_amp");
+  return JMT_OK;
+}
+
+extern "C" int jmt_amp_update(float* amp, float growth_factor, float backoff_factor,
+                              int growth_interval, void* stream) {
+  JMT_CHECK_ARG(amp && growth_interval >= 1, "jmt_amp_update: bad args");
+  hipLaunchKernelGGL(amp_update_kernel, dim3(1), dim3(64), 0, as_stream(stream), amp,
+                     growth_factor, backoff_factor, growth_interval);
+  JMT_LAUNCH_CHECK("jmt_amp_update");
+  return JMT_OK;
+}

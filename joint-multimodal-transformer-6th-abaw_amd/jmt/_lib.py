@@ -86,6 +86,10 @@ _PROTOS = {
     "jmt_vp_scatter": (c_int, [c_i64] + [c_vp] * 9 + [c_f, c_i64] + [c_vp] * 6),
     "jmt_vp_smooth": (c_int, [c_i64, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "jmt_vp_ccc": (c_int, [c_i64] + [c_vp] * 6),
+    "jmt_amp_check": (c_int, [c_i64, c_vp, c_vp, c_vp]),
+    "jmt_sgd_step_amp": (c_int, [c_i64, c_vp, c_vp, c_vp, c_f, c_f, c_f, c_f, c_int, c_int, c_vp,
+                                 c_vp, c_int, c_vp]),
+    "jmt_amp_update": (c_int, [c_vp, c_f, c_f, c_int, c_vp]),
     "jmt_gather_rows": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64,
                                 c_vp]),
     "jmt_sgd_step": (c_int, [c_i64, c_vp, c_vp, c_vp, c_f, c_f, c_f, c_f, c_int, c_int, c_f,

@@ -12,6 +12,7 @@ from typing import Iterable, List, Optional
 
 import torch
 
+from . import _lib
 from . import functional as F
 from . import ops
 
@@ -60,10 +61,55 @@ class FusedSGD:
                 p.grad = g
 
     @torch.no_grad()
+    def step_amp(self, amp_state: torch.Tensor):
+        """One step driven by a GradScaler's device state (unscale, skip on overflow).  Whether
+        the momentum buffer is initialised is then decided on the device (steps_taken), so plain
+        step() calls cannot follow scaled ones."""
+        self._amp = True
+        _lib.call("jmt_sgd_step_amp", self.numel, self.flat_p.data_ptr(), self.flat_g.data_ptr(),
+                  self.buf.data_ptr() if self.buf is not None else None, self.lr, self.momentum,
+                  self.dampening, self.weight_decay, int(self.nesterov), int(self.first),
+                  amp_state.data_ptr(),
+                  self.shadow.data_ptr() if self.shadow is not None else None,
+                  ops.dt(self.shadow) if self.shadow is not None else 1, ops.stream())
+
+    @torch.no_grad()
     def step(self, grad_scale: float = 1.0):
+        if getattr(self, "_amp", False):
+            raise RuntimeError("FusedSGD: step() after GradScaler steps (first-step state is on "
+                               "the device); keep using scaler.step(opt)")
         ops.sgd_step(self.flat_p, self.flat_g, self.buf, self.lr, self.momentum, self.dampening,
                      self.weight_decay, self.nesterov, self.first, grad_scale, self.shadow)
         self.first = False
+
+
+class GradScaler:
+    """torch.cuda.amp.GradScaler semantics (train.py:89,314-316) for FusedSGD with the whole
+    state on the device: `scaler.scale(loss).backward(); scaler.step(opt); scaler.update()` issue
+    kernels only (no host synchronisation; the step stays capturable into a hipGraph)."""
+
+    def __init__(self, init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
+                 backoff_factor: float = 0.5, growth_interval: int = 2000, device=None):
+        dev = torch.device(device) if device is not None else torch.device("cuda")
+        self.growth_factor, self.backoff_factor = growth_factor, backoff_factor
+        self.growth_interval = growth_interval
+        self.state = torch.tensor([init_scale, 1.0 / init_scale, 0.0, 0.0, 0.0],
+                                  dtype=torch.float32, device=dev)
+
+    def scale(self, loss: torch.Tensor) -> torch.Tensor:
+        return loss * self.state[0]
+
+    def step(self, opt: "FusedSGD"):
+        _lib.call("jmt_amp_check", opt.numel, opt.flat_g.data_ptr(), self.state.data_ptr(),
+                  ops.stream())
+        opt.step_amp(self.state)
+
+    def update(self):
+        _lib.call("jmt_amp_update", self.state.data_ptr(), self.growth_factor,
+                  self.backoff_factor, self.growth_interval, ops.stream())
+
+    def get_scale(self) -> float:
+        return float(self.state[0])
 
 
 def used_parameters(model_fn, params: Iterable[torch.nn.Parameter]):
