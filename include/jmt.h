@@ -87,6 +87,9 @@ int jmt_gemm_plan_splits(int ab_dtype, int M, int N, int K, int batch);
 /* development only: low byte = GEMM ablation flags (1 = skip MFMA, 2 = skip epilogue stores),
  * flags >> 8 = forced tile config (1 128x128, 5 256x256, 6 256x128, 7 128x256), 0 = off */
 void jmt_gemm_set_debug(int flags);
+/* development: per-block s_memrealtime stamps (entry, first K-tile, loop end, epilogue end) of
+ * the last launch made with debug flag 8; returns the number of blocks copied to host[4*n]. */
+int jmt_gemm_trace_read(uint64_t* host, int nblocks);
 
 /* ------------------------------------------------------------------ row-wise ops
  * Rows are `rows` vectors of length D at stride ld (elements). */

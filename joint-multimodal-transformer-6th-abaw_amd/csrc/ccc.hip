@@ -4,24 +4,13 @@
 // a GLOBAL-batch statistic as it is under the reference's DataParallel gather.
 //
 // Statistics are accumulated in double (one 1024-thread block; n = B*T elements per rank, a few
-// 10^4) — the kernel is latency-bound, never bandwidth-bound.
+// 10^4) — the kernel is latency-bound, never bandwidth-bound: one memory pass, register-cached.
 #include "common.h"
 
 namespace jmt {
 
 constexpr int CT = 1024;
 constexpr int MAXK = 64;   // digitize_num bins
-
-__device__ __forceinline__ double block_sum_d(double v, double* red) {
-  v = wave_sum_d(v);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
-  double s = 0.0;
-  for (int i = 0; i < CT / 64; ++i) s += red[i];
-  __syncthreads();
-  return s;
-}
 
 // numpy.linspace(lo, hi, k)[c] in float64, then cast to float32 (loss.py:14-16)
 __device__ __forceinline__ float bin_value(int c, int k, float lo, float hi) {
@@ -48,25 +37,73 @@ __device__ __forceinline__ float pred_value(const T* pred, int64_t i, int k, flo
   return e / s;
 }
 
+// three block sums at once (one LDS round trip)
+__device__ __forceinline__ void block_sum3_d(double& a, double& b, double& c, double* red) {
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  c = wave_sum_d(c);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[3 * w] = a;
+    red[3 * w + 1] = b;
+    red[3 * w + 2] = c;
+  }
+  __syncthreads();
+  a = b = c = 0.0;
+  for (int i = 0; i < CT / 64; ++i) {
+    a += red[3 * i];
+    b += red[3 * i + 1];
+    c += red[3 * i + 2];
+  }
+  __syncthreads();
+}
+
+// Two-pass (mean, then centred sums) statistics.  A thread's first RC elements are kept in
+// registers from pass 1 (all their loads issued together), so for n <= RC * CT (the JMT batches:
+// B*T = 19,200) pass 2 reads no memory; beyond that the rest is re-read.
+constexpr int RC = 24;
 template <typename T>
 __global__ __launch_bounds__(CT) void ccc_stats_kernel(int kind, int64_t n, int k, const T* pred,
                                                        const float* label, float ignore, float lo,
                                                        float hi, double* stats) {
-  __shared__ double red[CT / 64];
+  __shared__ double red[3 * (CT / 64)];
+  float xs[RC], ys[RC];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int64_t i = threadIdx.x + (int64_t)r * CT;
+    const bool in = i < n;
+    ys[r] = in ? label[i] : ignore;
+    xs[r] = in ? pred_value(pred, i, k, lo, hi) : 0.f;
+  }
   double c = 0, sx = 0, sy = 0;
-  for (int64_t i = threadIdx.x; i < n; i += CT) {
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int64_t i = threadIdx.x + (int64_t)r * CT;
+    if (i >= n || (kind == 1 && ys[r] == ignore)) continue;
+    c += 1.0;
+    sx += xs[r];
+    sy += ys[r];
+  }
+  for (int64_t i = threadIdx.x + (int64_t)RC * CT; i < n; i += CT) {
     const float y = label[i];
     if (kind == 1 && y == ignore) continue;
     c += 1.0;
     sx += pred_value(pred, i, k, lo, hi);
     sy += y;
   }
-  c = block_sum_d(c, red);
-  sx = block_sum_d(sx, red);
-  sy = block_sum_d(sy, red);
+  block_sum3_d(c, sx, sy, red);
   const double mx = c > 0 ? sx / c : 0.0, my = c > 0 ? sy / c : 0.0;
   double xx = 0, yy = 0, xy = 0;
-  for (int64_t i = threadIdx.x; i < n; i += CT) {
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int64_t i = threadIdx.x + (int64_t)r * CT;
+    if (i >= n || (kind == 1 && ys[r] == ignore)) continue;
+    const double dx = (double)xs[r] - mx, dy = (double)ys[r] - my;
+    xx += dx * dx;
+    yy += dy * dy;
+    xy += dx * dy;
+  }
+  for (int64_t i = threadIdx.x + (int64_t)RC * CT; i < n; i += CT) {
     const float y = label[i];
     if (kind == 1 && y == ignore) continue;
     const double dx = (double)pred_value(pred, i, k, lo, hi) - mx, dy = (double)y - my;
@@ -74,9 +111,7 @@ __global__ __launch_bounds__(CT) void ccc_stats_kernel(int kind, int64_t n, int 
     yy += dy * dy;
     xy += dx * dy;
   }
-  xx = block_sum_d(xx, red);
-  yy = block_sum_d(yy, red);
-  xy = block_sum_d(xy, red);
+  block_sum3_d(xx, yy, xy, red);
   if (threadIdx.x == 0) {
     stats[0] = c; stats[1] = mx; stats[2] = my;
     stats[3] = xx; stats[4] = yy; stats[5] = xy;

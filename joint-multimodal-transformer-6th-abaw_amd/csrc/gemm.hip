@@ -64,7 +64,7 @@ struct GemmParams {
   int tiles_m, tiles_n;
   int c_vec4;                   // C (and aux) 4-element groups aligned for 4-element stores
   int c_vec8;                   // C rows / base 16-B aligned (16-bit C: paired 16-B stores)
-  int dbg;                      // development ablations: 1 skip MFMA, 2 skip epilogue
+  int dbg;                      // development ablations: 1 skip MFMA, 2 skip epilogue, 8 trace
 };
 
 template <int BM_, int BN_, int WM_, int WN_, int KB_, int S_>
@@ -585,6 +585,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const GemmWor
   }
 }
 
+// development timeline probe (dbg & 8): wave 0 of each block stamps s_memrealtime (100 MHz) at
+// kernel entry, first K-tile landed, main loop done, epilogue done (scripts/gemm_timeline.py)
+constexpr int kTraceBlocks = 8192;
+__device__ uint64_t g_gemm_trace[kTraceBlocks * 4];
+__device__ __forceinline__ void trace_stamp(const GemmParams& p, int slot) {
+  if (!(p.dbg & 8) || threadIdx.x != 0) return;
+  const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  if (b < kTraceBlocks) g_gemm_trace[b * 4 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
 // One block per output tile (blockIdx.x, XCD-remapped), batch entry (blockIdx.y) and K split
 // (blockIdx.z).  (A persistent form — blocks capped at the resident slots, the next tile's first
 // K-tile prefetched under the epilogue — measured 3-5% slower: profiles/r01_gemm_persistent.txt.)
@@ -606,6 +616,7 @@ void gemm_kernel(GemmParams p) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int wm = wid / C::WN, wn = wid % C::WN;
+  trace_stamp(p, 0);
 
   f32x4 acc[C::TM][C::TN];
 #pragma unroll
@@ -624,6 +635,7 @@ void gemm_kernel(GemmParams p) {
         wait_vm(0);
       }
       __builtin_amdgcn_s_barrier();            // ... for every wave of the block
+      if (kt == 0) trace_stamp(p, 1);
       const char* img = smem + (kt & 1) * C::STAGE;
       if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
       __builtin_amdgcn_s_barrier();            // buffer (kt&1) free for tile kt+2
@@ -660,7 +672,9 @@ void gemm_kernel(GemmParams p) {
     if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(base, base + IA, wm, wn, acc);
   }
   __syncthreads();
+  trace_stamp(p, 2);
   gemm_epilogue<T, O, C>(p, cur, acc, lane, wm, wn);
+  trace_stamp(p, 3);
 }
 
 // split-K reduction + epilogue.  Vector form (N % 4 == 0, C 4-element aligned): one thread per 4
@@ -827,6 +841,14 @@ using namespace jmt;
 
 static int g_gemm_dbg = 0;
 static int g_gemm_cfg = 0;
+extern "C" int jmt_gemm_trace_read(uint64_t* host, int nblocks) {
+  if (nblocks > kTraceBlocks) nblocks = kTraceBlocks;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_trace), sizeof(uint64_t) * 4 * nblocks) !=
+          hipSuccess)
+    return -1;
+  return nblocks;
+}
 extern "C" void jmt_gemm_set_debug(int flags) { g_gemm_dbg = flags & 0xff; g_gemm_cfg = flags >> 8; }
 
 extern "C" int jmt_gemm_plan_splits(int ab_dtype, int M, int N, int K, int batch) {

@@ -51,6 +51,7 @@ _PROTOS = {
     "jmt_gemm_workspace_bytes": (C.c_size_t, [c_int, c_int, c_int, c_int]),
     "jmt_gemm_plan_splits": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "jmt_gemm_set_debug": (None, [c_int]),
+    "jmt_gemm_trace_read": (c_int, [c_vp, c_int]),
     "jmt_l2norm_fwd": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_i64, c_vp, c_f,
                                c_vp]),
     "jmt_l2norm_bwd": (c_int, [c_int, c_int, c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_i64, c_vp,
