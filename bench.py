@@ -74,11 +74,17 @@ def step_flops(B: int, T: int, Da: int = D_A, Dv: int = D_V, fc: bool = True,
 
 
 class GemmProbe:
-    """HIP-event timing of every launch of the dominant GEMM instance inside the timed region
-    (events recorded on the stream the kernels are launched on: torch's current stream)."""
+    """HIP-event timing of the dominant GEMM family over eager probe steps.  Each matching
+    launch of the step runs as usual; when it is idempotent (beta = 0, output aliasing no
+    input) it is then re-issued `reps` times back-to-back between ONE event pair on the
+    stream it is launched on (torch's current stream).  A pair around every single launch
+    reads 3-8 % above the kernel's rocprofv3 duration (the dispatch of the kernel after the
+    start marker is inside the pair: profiles/r01_event_check.txt); bracketing `reps`
+    launches spreads that over all of them."""
 
-    def __init__(self, key):
+    def __init__(self, key, reps: int = 8):
         self.key = key
+        self.reps = reps
         self.on = False
         self.events = []
         self.flops = []
@@ -87,12 +93,20 @@ class GemmProbe:
     def __call__(self, info, launch):
         if not self.on or (info["ab_dtype"], info["a_kmajor"], info["b_kmajor"]) != self.key:
             return launch()
+        s1 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        s1.record()
+        r = launch()
+        e1.record()
+        if info.get("beta", 0.0) != 0.0 or info.get("inplace", False):
+            return r
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
-        r = launch()
+        for _ in range(self.reps):
+            launch()
         e.record()
-        self.events.append((s, e))
+        self.events.append((s, e, s1, e1))
         self.flops.append(2.0 * info["M"] * info["N"] * info["K"] * info["batch"])
         ab = 4 if info["ab_dtype"] == 0 else 2
         cb = 4 if info["c_dtype"] == 0 else 2
@@ -103,8 +117,10 @@ class GemmProbe:
     def summary(self):
         if not self.events:
             return None
-        ms = [s.elapsed_time(e) for s, e in self.events]
+        ms = [s.elapsed_time(e) / self.reps for s, e, _, _ in self.events]
+        ms1 = [s1.elapsed_time(e1) for _, _, s1, e1 in self.events]
         return {"launches": len(ms), "avg_ms": sum(ms) / len(ms),
+                "avg_ms_single_pair": sum(ms1) / len(ms1),
                 "avg_flops": sum(self.flops) / len(self.flops),
                 "avg_bytes": sum(self.bytes) / len(self.bytes),
                 "total_ms": sum(ms)}
@@ -159,9 +175,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; JMT_DIST_BACKEND=gloo and the modulo only serve the rehearsal of the
+    # N>1 path with several ranks on a 1-GPU box (the driver's runs use RCCL, one rank per GPU)
+    backend = os.environ.get("JMT_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -248,13 +271,11 @@ def main():
         # the whole step as one hipGraph (jmt/graph.py): replay issues ~300 launches at once
         graphed = GraphedStep(step).capture(warmup=1)
         run = graphed.replay
-    elif not args.no_probe:
-        ops.set_launch_hook(probe)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    probe.on = not args.no_probe and not use_graph
+    probe.on = False
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = run()
@@ -265,10 +286,10 @@ def main():
     elapsed = time.perf_counter() - t0
     probe.on = False
     last_loss = float(loss.detach())
-    if use_graph and not args.no_probe:
-        # per-launch HIP events cannot sit inside the replayed graph: the dominant kernel is
-        # timed over `probe_steps` eager steps right after the timed region, with the same
-        # stream concurrency, on the streams its launches go to
+    if not args.no_probe:
+        # per-launch HIP events cannot sit inside the replayed graph (and would add host work to
+        # an eager timed region): the dominant kernel is timed over `probe_steps` eager steps
+        # right after the timed region, on the stream its launches go to
         ops.set_launch_hook(probe)
         probe.on = True
         for _ in range(args.probe_steps):
@@ -295,16 +316,17 @@ def main():
         traffic_src = os.path.relpath(tpath, REPO)
     if psum:
         achieved = psum["avg_flops"] / (psum["avg_ms"] * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "kernel": f"gemm_kernel<{args.dtype},Kmajor,Kmajor> (NT: all "
-                    "forward linears + attention scores)", "achieved": round(achieved, 1),
+        roofline = {"bound": "mfma", "kernel": f"gemm_kernel<{args.dtype},Kmajor,Kmajor> (NT: every forward "
+                    "linear: grouped in/out projections, FFN, FC head, regressors)", "achieved": round(achieved, 1),
                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                     "traffic_unit": "HBM bytes per launch (PMC)",
                     "traffic_source": traffic_src,
                     "algorithmic_bytes_per_launch": round(psum["avg_bytes"]),
-                    "launches_per_step": psum["launches"] // (args.probe_steps if use_graph else args.steps),
-                    "timed_over": ("eager probe steps after the timed region" if use_graph else "the timed region"),
+                    "launches_per_step": psum["launches"] // args.probe_steps,
+                    "timed_over": f"eager probe steps after the timed region; each launch re-issued {probe.reps}x between one event pair",
                     "avg_launch_us": round(psum["avg_ms"] * 1e3, 2),
+                    "avg_launch_us_single_pair": round(psum["avg_ms_single_pair"] * 1e3, 2),
                     "avg_gflop_per_launch": round(psum["avg_flops"] / 1e9, 3)}
     sfl = step_flops(B, T, **fl_kw)
     step_mfma = None

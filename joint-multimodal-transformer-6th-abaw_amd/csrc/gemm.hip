@@ -67,9 +67,13 @@ struct GemmParams {
   int dbg;                      // development ablations: 1 skip MFMA, 2 skip epilogue, 8 trace
 };
 
-template <int BM_, int BN_, int WM_, int WN_, int KB_, int S_>
+// PF: A-fragment prefetch distance in MFMA rows; PRIO: s_setprio(1) around each MFMA row;
+// SGB: sched_group_barrier pinning of each row's LDS reads ahead of its MFMAs.
+template <int BM_, int BN_, int WM_, int WN_, int KB_, int S_, int PF_ = 1, int PRIO_ = 0,
+          int SGB_ = 0>
 struct TileCfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, KB = KB_, S = S_;
+  static constexpr int PF = PF_, PRIO = PRIO_, SGB = SGB_;
   static constexpr int NT = 64 * WM * WN;          // threads per block
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -79,7 +83,10 @@ struct TileCfg {
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 using Cfg1 = TileCfg<128, 128, 2, 2, 128, 2>;
-using Cfg5 = TileCfg<256, 256, 2, 4, 128, 2>;
+// s_setprio(1) around each MFMA row: 2-4% faster on every step shape than the same tile without
+// it; a 2-row A prefetch with sched_group_barrier pinning gained nothing on top
+// (profiles/r01_gemm_sched.txt); on the 128x128 tile setprio measured +-2% (kept without)
+using Cfg5 = TileCfg<256, 256, 2, 4, 128, 2, 1, 1, 0>;
 // (deeper pipelines — 256x256 KB=64 with 3-4 stages, 128x128 with 3-4 stages — measured 0-40%
 // slower on every JMT shape: profiles/r01_gemm_pipeline_depth.txt)
 
@@ -266,6 +273,20 @@ __device__ __forceinline__ f32x4 read_frag32(const char* img, int rbase, int seg
 }
 
 
+__device__ __forceinline__ void sgb_ds_reads(int n) {   // sched_group_barrier needs literals
+  switch (n) {
+    case 1: __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); break;
+    case 2: __builtin_amdgcn_sched_group_barrier(0x100, 2, 0); break;
+    case 4: __builtin_amdgcn_sched_group_barrier(0x100, 4, 0); break;
+    case 5: __builtin_amdgcn_sched_group_barrier(0x100, 5, 0); break;
+    case 6: __builtin_amdgcn_sched_group_barrier(0x100, 6, 0); break;
+    case 8: __builtin_amdgcn_sched_group_barrier(0x100, 8, 0); break;
+    case 9: __builtin_amdgcn_sched_group_barrier(0x100, 9, 0); break;
+    case 10: __builtin_amdgcn_sched_group_barrier(0x100, 10, 0); break;
+    default: break;
+  }
+}
+
 template <typename T, bool AK, bool BK, class C>
 __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB, int wm, int wn,
                                              f32x4 (&acc)[C::TM][C::TN]) {
@@ -275,30 +296,43 @@ __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB,
     // so LDS latency hides behind TN MFMAs instead of stalling on lgkmcnt(0)
     typedef typename Frag16<T>::t F;
     constexpr int KS = C::KB / 64;
+    constexpr int NR = KS * C::TM;                 // MFMA rows of one K-tile
+    constexpr int PF = C::PF;                      // A rows read ahead
+    constexpr int BPF = PF < C::TM ? PF : C::TM - 1;   // B fragments read BPF rows ahead
     F fb[2][C::TN];
-    F fa[2];
+    F fa[PF + 1];
 #pragma unroll
     for (int j = 0; j < C::TN; ++j)
       fb[0][j] = read_frag16<T, BK, C::KB, C::BN>(imgB, wn * C::WTN + j * 16, 0);
-    fa[0] = read_frag16<T, AK, C::KB, C::BM>(imgA, wm * C::WTM, 0);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+    for (int r = 0; r < PF; ++r)
+      if (r < NR) fa[r] = read_frag16<T, AK, C::KB, C::BM>(imgA, wm * C::WTM + (r % C::TM) * 16,
+                                                          r / C::TM);
 #pragma unroll
-      for (int i = 0; i < C::TM; ++i) {
-        const int idx = ks * C::TM + i;
-        const int ni = (i + 1 < C::TM) ? i + 1 : 0;
-        const int nks = (i + 1 < C::TM) ? ks : ks + 1;
-        if (nks < KS) {
-          if (ni == 0) {
-#pragma unroll
-            for (int j = 0; j < C::TN; ++j)
-              fb[nks & 1][j] = read_frag16<T, BK, C::KB, C::BN>(imgB, wn * C::WTN + j * 16, nks);
-          }
-          fa[(idx + 1) & 1] = read_frag16<T, AK, C::KB, C::BM>(imgA, wm * C::WTM + ni * 16, nks);
-        }
+    for (int idx = 0; idx < NR; ++idx) {
+      const int ks = idx / C::TM, i = idx % C::TM;
+      int nreads = 0;
+      if (i == C::TM - BPF && ks + 1 < KS) {
 #pragma unroll
         for (int j = 0; j < C::TN; ++j)
-          acc[i][j] = mfma16(fb[ks & 1][j], fa[idx & 1], acc[i][j]);   // C^T tile
+          fb[(ks + 1) & 1][j] = read_frag16<T, BK, C::KB, C::BN>(imgB, wn * C::WTN + j * 16,
+                                                                 ks + 1);
+        nreads += BK ? C::TN : 2 * C::TN;
+      }
+      if (idx + PF < NR) {
+        const int r = idx + PF;
+        fa[r % (PF + 1)] = read_frag16<T, AK, C::KB, C::BM>(imgA, wm * C::WTM + (r % C::TM) * 16,
+                                                           r / C::TM);
+        nreads += AK ? 1 : 2;
+      }
+      if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j)
+        acc[i][j] = mfma16(fb[ks & 1][j], fa[idx % (PF + 1)], acc[i][j]);   // C^T tile
+      if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
+      if constexpr (C::SGB) {
+        sgb_ds_reads(nreads);                                                 // DS reads first
+        __builtin_amdgcn_sched_group_barrier(0x008, C::TN, 0);               // then the MFMAs
       }
     }
   } else {

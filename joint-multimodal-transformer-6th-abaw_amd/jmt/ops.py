@@ -103,7 +103,8 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
     if _launch_hook is not None:
         _launch_hook({"ab_dtype": ab_dtype, "c_dtype": c_dtype, "a_kmajor": bool(a_kmajor),
                       "b_kmajor": bool(b_kmajor), "M": M, "N": N, "K": K,
-                      "batch": batch0 * batch1}, launch)
+                      "batch": batch0 * batch1, "beta": beta,
+                      "inplace": any(p in list(c) for p in list(a) + list(b))}, launch)
     else:
         launch()
     return ws   # keep alive until the launch is ordered (caching allocator is stream-ordered)
