@@ -69,11 +69,13 @@ struct GemmParams {
 
 // PF: A-fragment prefetch distance in MFMA rows; PRIO: s_setprio(1) around each MFMA row;
 // SGB: sched_group_barrier pinning of each row's LDS reads ahead of its MFMAs.
+// OCC: minimum resident blocks per CU requested from the compiler (0: 2 x 256 threads' worth).
 template <int BM_, int BN_, int WM_, int WN_, int KB_, int S_, int PF_ = 1, int PRIO_ = 0,
-          int SGB_ = 0>
+          int SGB_ = 0, int OCC_ = 0>
 struct TileCfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, KB = KB_, S = S_;
   static constexpr int PF = PF_, PRIO = PRIO_, SGB = SGB_;
+  static constexpr int OCC = OCC_ > 0 ? OCC_ : (2 * 256 / (64 * WM_ * WN_) > 0 ? 2 * 256 / (64 * WM_ * WN_) : 1);
   static constexpr int NT = 64 * WM * WN;          // threads per block
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -87,6 +89,10 @@ using Cfg1 = TileCfg<128, 128, 2, 2, 128, 2>;
 // it; a 2-row A prefetch with sched_group_barrier pinning gained nothing on top
 // (profiles/r01_gemm_sched.txt); on the 128x128 tile setprio measured +-2% (kept without)
 using Cfg5 = TileCfg<256, 256, 2, 4, 128, 2, 1, 1, 0>;
+// 128x128 tiles with 64-B K-tiles at 4 resident blocks / CU (2 stages) or 3 (3 stages), so one
+// block's epilogue and loads overlap the others' MFMAs; chosen by occupancy_override()
+using Cfg10 = TileCfg<128, 128, 2, 2, 64, 2, 1, 1, 0, 4>;
+using Cfg11 = TileCfg<128, 128, 2, 2, 64, 3, 1, 1, 0, 3>;
 // (deeper pipelines — 256x256 KB=64 with 3-4 stages, 128x128 with 3-4 stages — measured 0-40%
 // slower on every JMT shape: profiles/r01_gemm_pipeline_depth.txt)
 
@@ -633,7 +639,7 @@ __device__ __forceinline__ void trace_stamp(const GemmParams& p, int slot) {
 // (blockIdx.z).  (A persistent form — blocks capped at the resident slots, the next tile's first
 // K-tile prefetched under the epilogue — measured 3-5% slower: profiles/r01_gemm_persistent.txt.)
 template <typename T, typename O, bool AK, bool BK, class C>
-__global__ __launch_bounds__(C::NT, 2 * 256 / C::NT > 0 ? 2 * 256 / C::NT : 1)
+__global__ __launch_bounds__(C::NT, C::OCC)
 void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BKE = C::KB / (int)sizeof(T);         // K elements per tile
@@ -795,6 +801,10 @@ template <typename T, typename O, bool AK, bool BK>
 static void launch_layout(const GemmParams& p, int cfg, dim3 grid, hipStream_t st) {
   switch (cfg) {
     case 5: launch_cfg<T, O, AK, BK, Cfg5>(p, grid, st); break;
+    case 10: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg10>(p, grid, st); break; }
+             [[fallthrough]];
+    case 11: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg11>(p, grid, st); break; }
+             [[fallthrough]];
     default: launch_cfg<T, O, AK, BK, Cfg1>(p, grid, st); break;
   }
 }
@@ -848,6 +858,17 @@ static double model_cost(const TileModel& t, int M, int N, int K, int batch, int
 static bool tile_ok(const TileModel& t, int M, int N) {
   const double pad = (double)((M + t.bm - 1) / t.bm * t.bm) * ((N + t.bn - 1) / t.bn * t.bn);
   return t.bm == 128 || (double)M * N >= 0.9 * pad;
+}
+
+// Launch families where a 128x128 tile at 3-4 resident blocks / CU (Cfg10 / Cfg11) beat the
+// planner's choice by 5-11% in two repeated step-shape sweeps (profiles/r01_gemm_occupancy.txt);
+// elsewhere they tie or lose, so they are selected by layout and shape, not by the cost model.
+static int occupancy_override(int ak, int bk, int M, int N, int K, int batch) {
+  if (!ak && !bk && batch >= 64 && M <= 512 && N <= 512 && K >= 128 && K <= 512)
+    return 11;                                                   // attn dK / dV
+  if (ak && !bk && batch == 1 && K >= 3072) return 11;           // K-concat stream dgrad
+  if (ak && !bk && batch >= 6 && K >= 1024 && K <= 2048 && M >= 4096) return 10;  // head dgrad
+  return 0;
 }
 
 static void plan(int dt, int M, int N, int K, int batch, int fixed_splits, int& cfg, int& splits) {
@@ -982,9 +1003,15 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
                   "jmt_gemm: split-K needs %zu workspace bytes", need);
   }
   int cfg = g_gemm_cfg;
+  if (dt == JMT_F32 && cfg >= 10) cfg = 1;   // occupancy configs: 16-bit only
   if (!cfg) {
     int s_unused;
     plan(dt, d->M, d->N, d->K, batch0 * batch1, splits, cfg, s_unused);
+    if (dt != JMT_F32 && splits == 1) {
+      const int t = occupancy_override(d->a_kmajor, d->b_kmajor, d->M, d->N, d->K,
+                                       batch0 * batch1);
+      if (t) cfg = t;
+    }
   }
   int bm, bn;
   cfg_tile(cfg, bm, bn);

@@ -1,0 +1,12 @@
+#!/bin/bash
+# GEMM occupancy experiment (cfg 10: 128x128 KB64 2-stage at 4 blocks/CU; cfg 11: 3-stage at 3
+# blocks/CU) vs the planner and cfg 1: forced-config kernel tests, then the step-shape bench.
+set -u
+OUT=gpurun_out; mkdir -p $OUT
+for c in 10 11; do
+  JMT_GEMM_CFG=$c timeout -k 10 200 python -m pytest tests/test_gpu_kernels.py -q -x --timeout 150 -p no:cacheprovider -k gemm > $OUT/kcfg$c.log 2>&1
+  rc=$?; echo "cfg $c tests: $(tail -1 $OUT/kcfg$c.log)"
+  if [ $rc -gt 1 ]; then exit $rc; fi
+done
+timeout -k 10 300 python scripts/bench_gemm_step.py --cfg 1 0 10 11 > $OUT/occ_step.log 2>&1 || exit $?
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; echo "smoke exit $?"; tail -1 $OUT/smoke.log
