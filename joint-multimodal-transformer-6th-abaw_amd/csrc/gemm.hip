@@ -93,6 +93,8 @@ using Cfg5 = TileCfg<256, 256, 2, 4, 128, 2, 1, 1, 0>;
 // block's epilogue and loads overlap the others' MFMAs; chosen by occupancy_override()
 using Cfg10 = TileCfg<128, 128, 2, 2, 64, 2, 1, 1, 0, 4>;
 using Cfg11 = TileCfg<128, 128, 2, 2, 64, 3, 1, 1, 0, 3>;
+// (8-wave 128x256 / 256x128 tiles with 64-B K-tiles, 3 stages, 2 blocks / CU measured 20-100%
+// slower on every step shape: profiles/r01_gemm_occupancy.txt)
 // (deeper pipelines — 256x256 KB=64 with 3-4 stages, 128x128 with 3-4 stages — measured 0-40%
 // slower on every JMT shape: profiles/r01_gemm_pipeline_depth.txt)
 
