@@ -558,6 +558,28 @@ __global__ __launch_bounds__(RB) void colsum_kernel(int64_t rows, int N, const T
   partials[(int64_t)blockIdx.x * N + c] = s;
 }
 
+// Narrow column sums (N <= 64, e.g. the 1-wide regressor output bias): NP = N rounded up to a
+// power of two columns x RB/NP row lanes per block, fixed-order LDS tree over the row lanes.
+template <typename T>
+__global__ __launch_bounds__(RB) void colsum_small_kernel(int64_t rows, int N, int NP,
+                                                          const T* dy, int64_t ld,
+                                                          float* partials) {
+  __shared__ float red[RB];
+  const int c = threadIdx.x % NP, ro = threadIdx.x / NP, rs = RB / NP;
+  const int64_t r0 = (int64_t)blockIdx.x * CS_ROWS;
+  const int64_t r1 = min(rows, r0 + CS_ROWS);
+  float s = 0.f;
+  if (c < N)
+    for (int64_t r = r0 + ro; r < r1; r += rs) s += to_f(dy[r * ld + c]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = rs / 2; h > 0; h >>= 1) {
+    if (ro < h) red[threadIdx.x] += red[threadIdx.x + h * NP];
+    __syncthreads();
+  }
+  if (ro == 0 && c < N) partials[(int64_t)blockIdx.x * N + c] = red[threadIdx.x];
+}
+
 // ------------------------------------------------------------------ strided copy
 // Row-contiguous copy / cast (both column strides 1, cols % 8 == 0, 16-B aligned rows when the
 // element is 16-bit; 8 elements per thread per step: 16-B loads of 16-bit, 2x16-B of f32).
@@ -759,6 +781,12 @@ extern "C" int jmt_softmax_bwd(int p_dt, int ds_dt, int64_t rows, int n, const v
   return JMT_OK;
 }
 
+static int next_pow2(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
 extern "C" int jmt_colsum_blocks(int64_t rows) { return (int)((rows + CS_ROWS - 1) / CS_ROWS); }
 
 extern "C" int jmt_colsum(int dt, int64_t rows, int N, const void* dy, int64_t ld, float* db,
@@ -776,6 +804,9 @@ extern "C" int jmt_colsum(int dt, int64_t rows, int N, const void* dy, int64_t l
       if (vec)
         hipLaunchKernelGGL((colsum_vec_kernel<T>), dim3(nblk, (N + 8 * ve - 1) / (8 * ve)),
                            dim3(RB), 0, st, rows, N, (const T*)dy, ld, partials);
+      else if (N <= 64)
+        hipLaunchKernelGGL((colsum_small_kernel<T>), dim3(nblk), dim3(RB), 0, st, rows, N,
+                           next_pow2(N), (const T*)dy, ld, partials);
       else
         hipLaunchKernelGGL((colsum_kernel<T>), dim3(nblk, (N + RB - 1) / RB), dim3(RB), 0, st,
                            rows, N, (const T*)dy, ld, partials));

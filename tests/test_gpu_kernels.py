@@ -294,6 +294,17 @@ def test_colsum_and_copy2d():
     assert (y.float() - x.t().bfloat16().float()).abs().max().item() == 0
 
 
+@pytest.mark.parametrize("N,ld", [(1, 1), (3, 5), (64, 64)])
+def test_colsum_narrow(N, ld):
+    """Narrow column sums (the regressor output biases): small-N kernel, ragged row count."""
+    g = torch.Generator(device=DEV).manual_seed(13)
+    dy = torch.randn(19201, ld, device=DEV, generator=g).bfloat16()
+    db = torch.zeros(N, device=DEV)
+    ops.colsum(dy, ld, 19201, N, db, beta_acc=False)
+    ref = dy[:, :N].float().sum(0)
+    assert (db - ref).abs().max().item() < 1e-3
+
+
 def test_sgd_matches_torch_nesterov():
     g = torch.Generator(device=DEV).manual_seed(12)
     p = torch.randn(10007, device=DEV, generator=g)
