@@ -93,6 +93,7 @@ using Cfg5 = TileCfg<256, 256, 2, 4, 128, 2, 1, 1, 0>;
 // block's epilogue and loads overlap the others' MFMAs; chosen by occupancy_override()
 using Cfg10 = TileCfg<128, 128, 2, 2, 64, 2, 1, 1, 0, 4>;
 using Cfg11 = TileCfg<128, 128, 2, 2, 64, 3, 1, 1, 0, 3>;
+// (without s_setprio the two measured the same: profiles/r01_gemm_occupancy.txt)
 // (8-wave 128x256 / 256x128 tiles with 64-B K-tiles, 3 stages, 2 blocks / CU measured 20-100%
 // slower on every step shape: profiles/r01_gemm_occupancy.txt)
 // (deeper pipelines — 256x256 KB=64 with 3-4 stages, 128x128 with 3-4 stages — measured 0-40%
@@ -863,13 +864,15 @@ static bool tile_ok(const TileModel& t, int M, int N) {
 }
 
 // Launch families where a 128x128 tile at 3-4 resident blocks / CU (Cfg10 / Cfg11) beat the
-// planner's choice by 5-11% in two repeated step-shape sweeps (profiles/r01_gemm_occupancy.txt);
+// planner's choice by 3-11% in repeated step-shape sweeps (profiles/r01_gemm_occupancy.txt);
 // elsewhere they tie or lose, so they are selected by layout and shape, not by the cost model.
 static int occupancy_override(int ak, int bk, int M, int N, int K, int batch) {
   if (!ak && !bk && batch >= 64 && M <= 512 && N <= 512 && K >= 128 && K <= 512)
     return 11;                                                   // attn dK / dV
   if (ak && !bk && batch == 1 && K >= 3072) return 11;           // K-concat stream dgrad
   if (ak && !bk && batch >= 6 && K >= 1024 && K <= 2048 && M >= 4096) return 10;  // head dgrad
+  if (ak && bk && batch >= 3 && N >= 1536 && K == 512 && M >= 4096) return 11;   // grouped qkv
+  if (ak && !bk && batch == 6 && K == 512 && M >= 4096) return 11;    // cross-attn dgrad
   return 0;
 }
 

@@ -1,6 +1,6 @@
 #!/bin/bash
-# GEMM occupancy experiments (cfg 10/11: 128x128 KB64 at 4/3 blocks per CU; cfg 12/13: 8-wave
-# 128x256 / 256x128 KB64 3-stage at 2 blocks per CU) vs the planner: forced-config kernel tests,
+# GEMM occupancy experiment (cfg 10/11: 128x128 KB64 at 4/3 blocks per CU) vs the planner and
+# cfg 1: forced-config kernel tests, the step-shape microbenchmark, then smoke().
 set -u
 OUT=gpurun_out; mkdir -p $OUT
 for c in 10 11; do
