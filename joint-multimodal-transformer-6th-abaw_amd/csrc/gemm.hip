@@ -866,7 +866,10 @@ static bool tile_ok(const TileModel& t, int M, int N) {
 // Launch families where a 128x128 tile at 3-4 resident blocks / CU (Cfg10 / Cfg11) beat the
 // planner's choice by 3-11% in repeated step-shape sweeps (profiles/r01_gemm_occupancy.txt);
 // elsewhere they tie or lose, so they are selected by layout and shape, not by the cost model.
-static int occupancy_override(int ak, int bk, int M, int N, int K, int batch) {
+static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, int splits) {
+  if (!ak && !bk && M >= 1536 && N >= 512 && batch >= 3 && K >= 8192)
+    return 10;                                                   // split-K qkv wgrad
+  if (splits > 1) return 0;
   if (!ak && !bk && batch >= 64 && M <= 512 && N <= 512 && K >= 128 && K <= 512)
     return 11;                                                   // attn dK / dV
   if (ak && !bk && batch == 1 && K >= 3072) return 11;           // K-concat stream dgrad
@@ -1012,9 +1015,9 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   if (!cfg) {
     int s_unused;
     plan(dt, d->M, d->N, d->K, batch0 * batch1, splits, cfg, s_unused);
-    if (dt != JMT_F32 && splits == 1) {
+    if (dt != JMT_F32 && (cfg == 1 || splits == 1)) {   // same 128x128 split plan when split
       const int t = occupancy_override(d->a_kmajor, d->b_kmajor, d->M, d->N, d->K,
-                                       batch0 * batch1);
+                                       batch0 * batch1, splits);
       if (t) cfg = t;
     }
   }
