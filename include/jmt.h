@@ -176,8 +176,11 @@ int jmt_copy2d(int src_dt, int dst_dt, int64_t rows, int64_t cols, const void* s
  * kind 0: losses/loss.py:8-32 CCCLoss (digitize_num k; k>1: pred is (n,k) logits, softmax over
  *         bins = linspace(range) first)
  * kind 1: losses/CCCLoss.py:4-43 CCCLoss(ignore) (labels == ignore are masked; the ccc is
- *         divided by the pre-mask batch size `bs`)
- * Local statistics (double[8]: n, mean_x, mean_y, M2x, M2y, Cxy, 0, 0) of this rank's elements;
+ *         divided by the pre-mask batch size `bs`: bs >= 1 as given — size(0) of the (1, B*T)
+ *         view of train.py:303-307, the same on every rank —, bs < 0 = 1-D predictions: the
+ *         gathered size(0) = sum over ranks of the pre-mask counts)
+ * Local statistics (double[8]: n, mean_x, mean_y, M2x, M2y, Cxy, pre-mask count, 0) of this
+ * rank's elements;
  * several ranks' statistics are combined exactly (Chan) by jmt_ccc_finish, which writes the loss
  * (fp32 scalar) and 8 doubles of gradient coefficients {c0, c1, c2, mean_x, mean_y, valid, 0, 0}
  * used by jmt_ccc_bwd: dL/dx_i = grad_loss * (c0 + c1 (x_i - mean_x) + c2 (y_i - mean_y)). */

@@ -115,16 +115,25 @@ __global__ __launch_bounds__(CT) void ccc_stats_kernel(int kind, int64_t n, int 
   if (threadIdx.x == 0) {
     stats[0] = c; stats[1] = mx; stats[2] = my;
     stats[3] = xx; stats[4] = yy; stats[5] = xy;
-    stats[6] = 0; stats[7] = 0;
+    stats[6] = (double)n;                         // pre-mask element count (global bs, below)
+    stats[7] = 0;
   }
 }
 
 // Combine rank statistics in fixed rank order, then loss + gradient coefficients.
 //   coef = {c0, c1, c2, mean_x, mean_y, valid, 0, 0};  dL/dx_i = c0 + c1 (x_i - mx) + c2 (y_i - my)
-__global__ void ccc_finish_kernel(int kind, int world, const double* st, int64_t bs, float eps,
+// bs (kind 1, CCCLoss.py:17 `y_pred.size(0)` before masking): bs >= 1 is used as given (the
+// (1, B*T) view of train.py:303-307: size(0) is 1 on every rank and after the gather); bs < 0
+// means "1-D predictions": size(0) of the GATHERED batch = the sum of the ranks' pre-mask counts.
+__global__ void ccc_finish_kernel(int kind, int world, const double* st, int64_t bs_in, float eps,
                                   float* loss, double* coef) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   double n = st[0], mx = st[1], my = st[2], Sxx = st[3], Syy = st[4], Sxy = st[5];
+  double bsd = (double)bs_in;
+  if (bs_in < 0) {
+    bsd = 0.0;
+    for (int r = 0; r < world; ++r) bsd += st[8 * r + 6];
+  }
   for (int r = 1; r < world; ++r) {
     const double* s = st + 8 * r;
     const double nb = s[0];
@@ -179,12 +188,12 @@ __global__ void ccc_finish_kernel(int kind, int world, const double* st, int64_t
     const float y_std = sqrtf((float)Sxx / (fn - 1.f));   // std(y_pred)
     const float dm = (float)mx - (float)my;
     const float den = x_std * x_std + y_std * y_std + dm * dm + 1e-8f;
-    const float ccc = 2.f * (float)Sxy / (den * (float)bs);
+    const float ccc = 2.f * (float)Sxy / (den * (float)bsd);
     *loss = 1.f - ccc;
     const double nm1 = n - 1.0;
     const double D = Syy / nm1 + Sxx / nm1 + (mx - my) * (mx - my) + 1e-8;
-    const double dccc_dSxy = 2.0 / (D * (double)bs);
-    const double g = -2.0 * Sxy / (D * D * (double)bs);
+    const double dccc_dSxy = 2.0 / (D * bsd);
+    const double g = -2.0 * Sxy / (D * D * bsd);
     const double dccc_dSxx = g / nm1;
     const double dccc_dmx = g * 2.0 * (mx - my);
     coef[0] = -dccc_dmx / n;

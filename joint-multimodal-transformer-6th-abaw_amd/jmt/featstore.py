@@ -33,7 +33,7 @@ _NP = {"float32": np.float32, "float16": np.float16}
 
 
 class FeatureStoreWriter:
-    def __init__(self, path: str, modalities: Dict[str, int], dtype: str = "float16"):
+    def __init__(self, path: str, modalities: Dict[str, int], dtype: str = "float32"):
         assert dtype in _NP
         os.makedirs(path, exist_ok=True)
         self.path, self.dims, self.dtype = path, dict(modalities), dtype
@@ -67,7 +67,7 @@ class FeatureStoreWriter:
 
     @staticmethod
     def from_npy_tree(path: str, root: str, modality: str = "wavlm", dim: int = 768,
-                      dtype: str = "float16", videos: Optional[Sequence[str]] = None,
+                      dtype: str = "float32", videos: Optional[Sequence[str]] = None,
                       lengths: Optional[Dict[str, int]] = None):
         """Pack create_wavlm_audio_feat.py's tree <root>/<video>/<k>.npy (k = 1..length)."""
         w = FeatureStoreWriter(path, {modality: dim}, dtype)

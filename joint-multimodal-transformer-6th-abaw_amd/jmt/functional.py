@@ -64,10 +64,26 @@ def _vec(dtype: torch.dtype) -> int:
 
 # ------------------------------------------------------------------------- weight shadows
 def weight_as(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
-    """fp32 parameter -> contiguous compute-dtype copy, cached on the parameter itself and
-    re-cast only when the parameter's version / storage changes."""
+    """fp32 parameter -> contiguous compute-dtype copy.
+
+    * Parameters owned by FusedSGD with a shadow of this dtype read that shadow (the SGD kernel
+      rewrites it in the same pass as the fp32 weight, without bumping `_version`).  An in-place
+      write from anywhere else (load_state_dict, copy_, ...) bumps `_version`: the shadow is then
+      re-cast IN PLACE, so the optimizer keeps updating the buffer the forward reads.
+    * Parameters owned by FusedSGD without a matching shadow are never cached: the fused step
+      changes them without a version bump, so a cached cast would freeze them.  (A captured
+      hipGraph then replays the cast every step.)
+    * Anything else is cached on the parameter and re-cast when its version / storage changes."""
     if w.dtype == dtype:
         return w if w.is_contiguous() else w.contiguous()
+    fused = getattr(w, "_jmt_fused", None)
+    if fused is not None:
+        if fused[0] is not None and fused[0].dtype == dtype:
+            if fused[1] != w._version or fused[2] != w.data_ptr():
+                ops.cast(w.detach(), dtype, out=fused[0])
+                w._jmt_fused = (fused[0], w._version, w.data_ptr())
+            return fused[0]
+        return ops.cast(w.detach(), dtype)
     ent = getattr(w, "_jmt_shadow", None)
     if ent is not None and ent[0] == w._version and ent[1] == dtype and ent[2] == w.data_ptr():
         return ent[3]
@@ -76,9 +92,11 @@ def weight_as(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return t
 
 
-def register_shadow(w: torch.Tensor, shadow: torch.Tensor):
-    """Used by the fused optimizer, which rewrites `shadow` in the same kernel as `w`."""
-    w._jmt_shadow = (w._version, shadow.dtype, w.data_ptr(), shadow)
+def register_shadow(w: torch.Tensor, shadow: Optional[torch.Tensor]):
+    """Used by the fused optimizer, which rewrites `shadow` (or nothing: None) in the same kernel
+    as `w`: from now on `w` changes without a version bump (see weight_as)."""
+    w._jmt_fused = (shadow, w._version, w.data_ptr())
+    w._jmt_shadow = None
 
 
 def _grad_buffer(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -303,21 +321,33 @@ class MLPFn(Function):
         y = L.like(nout, odt)
         _linear_fwd([h], ldh, L.rows, hid, W2, 0, nout, b2, y, _ld(y, L.perm), cd)
         ctx.save_for_backward(W1, b1, W2, b2, L.t, h)
-        ctx.meta = (cd, L, x.dtype)
+        ctx.meta = (cd, L, x.dtype, odt)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         W1, b1, W2, b2, xin, h = ctx.saved_tensors
-        cd, L, xdt = ctx.meta
+        cd, L, xdt, odt = ctx.meta
         hid, nout = W1.shape[0], W2.shape[0]
         Gy = _match(gy, Rows(L.like(nout, cd)), cd)
         H = Rows(h)
         dh = L.like(hid, cd)
         ldh = _ld(dh, L.perm)
         _dgrad(Gy, nout, W2, 0, cd, [dh], ldh, 1, hid, aux=h, ldaux=H.ld)
-        _wgrad(Gy, nout, [h], H.ld, hid, W2, 0, cd)
-        _bgrad(Gy, nout, b2, 0)
+        if odt == torch.float32 and cd != torch.float32 and nout <= 16:
+            # fp32 output (the V/A regressors' last layer, two_transformers.py:104-114): its
+            # weight / bias gradients are sums over all rows of the fp32 loss gradient, which
+            # nearly cancel (sum_i dL/dx_i = n c0 for the CCC): summing a 16-bit rounded copy
+            # would cost up to ~20 % relative error, so they are reduced from fp32 dY and an fp32
+            # copy of the (small) hidden activations with the exact-f32 MFMA GEMM.
+            G32 = _match(gy, Rows(L.like(nout, torch.float32)), torch.float32)
+            h32 = _cast_keep_layout(h, torch.float32)
+            H32 = Rows(h32)
+            _wgrad(G32, nout, [H32.t], H32.ld, hid, W2, 0, torch.float32)
+            _bgrad(G32, nout, b2, 0)
+        else:
+            _wgrad(Gy, nout, [h], H.ld, hid, W2, 0, cd)
+            _bgrad(Gy, nout, b2, 0)
         Gh = Rows(dh)
         dx = None
         if ctx.needs_input_grad[5]:
@@ -716,5 +746,8 @@ def ccc_loss(pred, label, eps=1e-8, digitize_num=1, rng=(-1.0, 1.0), group=None)
 
 
 def ccc_loss_ignore(pred, label, ignore=-5.0, group=None):
-    bs = pred.shape[0]
+    # losses/CCCLoss.py:17 divides by y_pred.size(0) of the (gathered) batch: for the (1, B*T)
+    # view of train.py:303-307 that is 1 on every rank; for 1-D predictions the gathered size(0)
+    # is the sum of the ranks' sizes (-1: summed on the device by jmt_ccc_finish)
+    bs = pred.shape[0] if pred.dim() >= 2 else -1
     return CCCLossFn.apply(pred, label, 1, 1, float(ignore), -1.0, 1.0, 0.0, int(bs), group)

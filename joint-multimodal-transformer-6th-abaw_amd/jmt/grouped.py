@@ -378,10 +378,12 @@ class CrossAttention6Fn(Function):
         dY = torch.zeros(S, B, T, E, dtype=cd, device=dev) if any(
             not any(q == s or k == s for _, q, k in pairs) for s in range(S)) else \
             torch.empty(S, B, T, E, dtype=cd, device=dev)
+        keep = []     # the 16-bit weight copies must outlive the launches that read them
         for s in range(S):
             a_ptrs, b_ptrs = [], []
             for i, (m, q, k) in enumerate(pairs):
                 Wc = weight_as(M[m][0], cd)
+                keep.append(Wc)
                 if q == s:
                     a_ptrs.append(_ptr(dQKV, i * R * 3 * E))
                     b_ptrs.append(_ptr(Wc, 0))

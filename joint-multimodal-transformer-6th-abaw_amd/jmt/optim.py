@@ -50,8 +50,9 @@ class FusedSGD:
                 self._gviews.append(g)
         if self.shadow is not None:
             ops.cast(self.flat_p, self.shadow.dtype, out=self.shadow)
-            for p, off in zip(self.params, offs):
-                F.register_shadow(p, self.shadow[off:off + p.numel()].view_as(p))
+        for p, off in zip(self.params, offs):
+            F.register_shadow(p, self.shadow[off:off + p.numel()].view_as(p)
+                              if self.shadow is not None else None)
         self.first = True
 
     def zero_grad(self, set_to_none: bool = False):

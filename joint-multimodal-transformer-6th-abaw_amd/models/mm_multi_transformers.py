@@ -11,6 +11,7 @@ import torch.nn as nn
 from jmt import functional as F
 from jmt import grouped
 from jmt import streams
+from jmt import taps
 from jmt.nn import Linear, LayerNorm, MLP, MultiheadAttention
 
 __all__ = ["Attention", "SequentialEncoder", "TransformerEncoderBlock",
@@ -122,6 +123,9 @@ class MultimodalTransformer_w_JR(nn.Module):
         v, p, j = streams.run_parallel([lambda: self.visual_encoder(v),
                                         lambda: self.physiological_encoder(p),
                                         lambda: self.joint_representation_encoder(j)], dev)
+        taps.record("enc.visual_encoder", v, True)
+        taps.record("enc.physiological_encoder", p, True)
+        taps.record("enc.joint_representation_encoder", j, True)
 
         # six cross-attentions (:142-167, key is value in every call); each module is applied
         # to the same query twice, so its query projection is computed once
@@ -140,6 +144,8 @@ class MultimodalTransformer_w_JR(nn.Module):
                 r_v[1],      # CA_v(v, j)
                 r_pv[1],     # CA_pv(j, p)
                 r_p[1]]      # CA_p(p, j)
+        for i, o in enumerate(outs):
+            taps.record(f"ca.{i}", o, True)
         if self.output_format == "SELF_ATTEN":
             return self._self_atten_head(outs)
         # FC head (:201-211): torch.cat of the 6 outputs never materialised (K-concat GEMM)
@@ -153,8 +159,11 @@ class MultimodalTransformer_w_JR(nn.Module):
         for lv, lp, lj in zip(self.visual_encoder.layers, self.physiological_encoder.layers,
                               self.joint_representation_encoder.layers):
             X = grouped.encoder_group(X, [lv, lp, lj], self.num_heads)
+        taps.record_stacked(["enc.visual_encoder", "enc.physiological_encoder",
+                             "enc.joint_representation_encoder"], X)
         O6 = grouped.cross_attention6(X, [self.cross_attention_v, self.cross_attention_p,
                                           self.cross_attention_pv], self.num_heads)
+        taps.record_stacked([f"ca.{i}" for i in range(O6.shape[0])], O6)
         if self.output_format == "SELF_ATTEN":
             return self._self_atten_head([O6[i].permute(1, 0, 2) for i in range(6)])
         # FC head (:201-211): seq-first (T, B, 1024), as the reference returns it

@@ -6,6 +6,7 @@ import torch.nn as nn
 
 from jmt import functional as F
 from jmt import streams
+from jmt import taps
 from jmt.nn import Linear
 
 from .mm_multi_transformers import (Attention, SequentialEncoder, TransformerEncoderBlock,
@@ -42,9 +43,13 @@ class MultimodalTransformer_wo_JR(nn.Module):
         v, p = streams.run_parallel([lambda: self.visual_encoder(visual_features),
                                      lambda: self.physiological_encoder(physiological_features)],
                                     dev)
+        taps.record("enc.visual_encoder", v)
+        taps.record("enc.physiological_encoder", p)
         vt, pt = v.permute(1, 0, 2), p.permute(1, 0, 2)
         ov, op = streams.run_parallel([lambda: self.cross_attention_v(vt, pt, pt)[0],
                                        lambda: self.cross_attention_p(pt, vt, vt)[0]], dev)
         ov, op = ov.permute(1, 0, 2), op.permute(1, 0, 2)
+        taps.record("ca.0", ov)
+        taps.record("ca.1", op)
         assert self.output_format == 'FC', self.output_format
         return F.linear((ov, op), self.final_layer.weight, self.final_layer.bias)

@@ -7,6 +7,7 @@ import torch
 from torch import nn
 
 from jmt import functional as F
+from jmt import taps
 from jmt.nn import Linear, MLP
 
 from .mm_multi_transformers import MultimodalTransformer_w_JR
@@ -75,6 +76,8 @@ class Two_transformers(nn.Module):
         if self.linear is not None:
             video = self.linear(video)           # :120-121
         av = self.mm_transformer(video, audio)
+        taps.record("head", av, self.joint_modalities == 'TRANSFORMER' and
+                    self.output_format == 'FC')
         # regressors in fp32 out (predictions feed the fp32 CCC statistics)
         vouts = self.vregressor(av, out_dtype=torch.float32).squeeze(2)
         aouts = self.aregressor(av, out_dtype=torch.float32).squeeze(2)

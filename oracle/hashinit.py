@@ -45,16 +45,33 @@ def uniform(name: str, shape, lo: float, hi: float) -> np.ndarray:
     return (lo + (hi - lo) * uniform01(name, n)).reshape(shape).astype(np.float32)
 
 
+# Gains on the nn.Linear bound for selected 2-D weights (round 2).  With the plain bound the
+# attention scores have std ~0.3, softmax is nearly flat over T keys, every attention output is
+# ~the mean of V and the predictions are near-constant (spread 1e-3): a broken attention would
+# not show.  x4 on the packed in_proj weights (scores x16: std ~5, peaked softmax) and x3 on the
+# head / regressor output layers give predictions with O(0.3-1.6) spread on every golden case.
+GAINS = (("in_proj_weight", 4.0), ("out_layer1.weight", 3.0), ("final_layer.weight", 3.0),
+         ("regressor.3.weight", 3.0), ("mm_transformer.fc.weight", 3.0))
+
+
+def gain(name: str) -> float:
+    for pat, g in GAINS:
+        if pat in name:
+            return g
+    return 1.0
+
+
 def param_value(name: str, shape) -> np.ndarray:
     """Deterministic value for a parameter of the given state_dict name and shape.
 
-    * 2-D weights: U(-1/sqrt(fan_in), 1/sqrt(fan_in)), fan_in = shape[1] (nn.Linear convention).
+    * 2-D weights: U(-g/sqrt(fan_in), g/sqrt(fan_in)), fan_in = shape[1] (nn.Linear convention),
+      g = gain(name) (1 except the GAINS above).
     * LayerNorm weight ('layer_norm*.weight'): 1 + U(-0.1, 0.1) so the affine path is exercised.
     * any other 1-D tensor (biases, LN bias): U(-0.1, 0.1).
     """
     shape = tuple(int(s) for s in shape)
     if len(shape) == 2:
-        b = 1.0 / np.sqrt(shape[1])
+        b = gain(name) / np.sqrt(shape[1])
         return uniform("w:" + name, shape, -b, b)
     if "layer_norm" in name and name.endswith("weight"):
         return (1.0 + uniform("w:" + name, shape, -0.1, 0.1)).astype(np.float32)

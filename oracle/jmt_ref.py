@@ -23,17 +23,86 @@ import torch
 P = Dict[str, torch.Tensor]
 
 
+# ---------------------------------------------------------------- 16-bit storage emulation ----
+# emulate_storage(torch.bfloat16 / torch.float16) makes the restatement round every tensor the HIP
+# path stores in the compute dtype (GEMM operands and outputs, LayerNorm / L2-norm outputs,
+# attention probabilities) — in the forward value AND in the gradient flowing back through that
+# point — while all arithmetic stays fp32 (fp32 MFMA accumulation, fp32 statistics).  It is the
+# error model of the 16-bit parity tests: it measures what plain 16-bit storage of the reference's
+# math costs on a given input, independently of the HIP kernels (tests/test_gpu_models.py).
+_EMU = {"dtype": None}
+
+
+class _Round(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, t, dtype):
+        ctx.dtype = dtype
+        return t.to(dtype).to(t.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.dtype).to(g.dtype), None
+
+
+class _AttnCore16(torch.autograd.Function):
+    """softmax(scale Q K^T) V with 16-bit storage emulated the way a flash-style kernel stores
+    it: scores / softmax in fp32, P rounded for P V, O rounded; backward with
+    Delta = rowsum(dO o O) from the 16-bit dO and O, dS = P o (dP - Delta) in fp32 then rounded,
+    P rounded for dV = P^T dO (the standard flash-attention backward formula)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale, dtype):
+        r = lambda t: t.to(dtype).to(torch.float32)
+        P = torch.softmax(torch.bmm(q, k.transpose(1, 2)) * scale, dim=-1)
+        o = r(torch.bmm(r(P), v))
+        ctx.save_for_backward(q, k, v, P, o)
+        ctx.scale, ctx.dtype = scale, dtype
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, P, o = ctx.saved_tensors
+        r = lambda t: t.to(ctx.dtype).to(torch.float32)
+        do = r(do)
+        dP = torch.bmm(do, v.transpose(1, 2))
+        delta = (do * o).sum(-1, keepdim=True)
+        dS = r(P * (dP - delta) * ctx.scale)
+        return (r(torch.bmm(dS, k)), r(torch.bmm(dS.transpose(1, 2), q)),
+                r(torch.bmm(r(P).transpose(1, 2), do)), None, None)
+
+
+def rnd(t):
+    d = _EMU["dtype"]
+    return t if d is None else _Round.apply(t, d)
+
+
+class emulate_storage:
+    """`with emulate_storage(torch.bfloat16): ...` (None = exact fp32)."""
+
+    def __init__(self, dtype):
+        self.dtype = dtype
+
+    def __enter__(self):
+        self.prev = _EMU["dtype"]
+        _EMU["dtype"] = self.dtype
+        return self
+
+    def __exit__(self, *a):
+        _EMU["dtype"] = self.prev
+
+
 # ---------------------------------------------------------------- primitives ------------------
 
-def linear(x, W, b):
+def linear(x, W, b, out_round: bool = True):
     """nn.Linear: y = x W^T + b (models/fc_layer.py:6-12, two_transformers.py:56)."""
-    return torch.matmul(x, W.t()) + b
+    y = torch.matmul(rnd(x), rnd(W).t()) + b
+    return rnd(y) if out_round else y
 
 
 def l2_normalize(x, eps: float = 1e-12):
     """F.normalize(x, p=2, dim=-1, eps=1e-12) (models/two_transformers.py:118-119)."""
     n = torch.sqrt((x * x).sum(-1, keepdim=True))
-    return x / torch.clamp(n, min=eps)
+    return rnd(x / torch.clamp(n, min=eps))
 
 
 def layer_norm(x, g, b, eps: float = 1e-5):
@@ -41,7 +110,7 @@ def layer_norm(x, g, b, eps: float = 1e-5):
     mu = x.mean(-1, keepdim=True)
     xc = x - mu
     var = (xc * xc).mean(-1, keepdim=True)
-    return xc * torch.rsqrt(var + eps) * g + b
+    return rnd(xc * torch.rsqrt(var + eps) * g + b)
 
 
 def mha(q_in, k_in, v_in, p: P, pre: str, num_heads: int):
@@ -63,11 +132,15 @@ def mha(q_in, k_in, v_in, p: P, pre: str, num_heads: int):
     S = k.shape[0]
     H = num_heads
     dh = E // H
-    q = q.reshape(L, N * H, dh).transpose(0, 1) * (1.0 / math.sqrt(dh))
+    q = q.reshape(L, N * H, dh).transpose(0, 1)
     k = k.reshape(S, N * H, dh).transpose(0, 1)
     v = v.reshape(S, N * H, dh).transpose(0, 1)
-    a = torch.softmax(torch.bmm(q, k.transpose(1, 2)), dim=-1)
-    o = torch.bmm(a, v).transpose(0, 1).reshape(L, N, E)
+    if _EMU["dtype"] is None:
+        a = torch.softmax(torch.bmm(q * (1.0 / math.sqrt(dh)), k.transpose(1, 2)), dim=-1)
+        o = torch.bmm(a, v)
+    else:
+        o = _AttnCore16.apply(q, k, v, 1.0 / math.sqrt(dh), _EMU["dtype"])
+    o = o.transpose(0, 1).reshape(L, N, E)
     return linear(o, p[pre + "out_proj.weight"], p[pre + "out_proj.bias"])
 
 
@@ -90,7 +163,14 @@ def encoder_block(x, p: P, pre: str, num_heads: int, num_layers: int):
 
 # ---------------------------------------------------------------- fusion models --------------
 
-def w_jr_forward(visual, phys, p: P, pre: str, H: int, L: int, output_format: str):
+def _tap(taps, name, t, seq_first):
+    """Record an intermediate as (tensor, seq_first); (B, T, F) is the canonical layout (test
+    infrastructure: the golden generator taps the same points of the reference with hooks)."""
+    if taps is not None:
+        taps[name] = (t, seq_first)
+
+
+def w_jr_forward(visual, phys, p: P, pre: str, H: int, L: int, output_format: str, taps=None):
     """MultimodalTransformer_w_JR.forward (models/mm_multi_transformers.py:118-214).
     visual/phys: (B, T, 512).  FC -> (T, B, 1024); SELF_ATTEN -> (B, T, 512)."""
     jr = linear(torch.cat((visual, phys), dim=2), p[pre + "out_layer_pv.weight"],
@@ -101,6 +181,9 @@ def w_jr_forward(visual, phys, p: P, pre: str, H: int, L: int, output_format: st
     v = encoder_block(v, p, pre + "visual_encoder.", H, L)                      # :132-136
     a = encoder_block(a, p, pre + "physiological_encoder.", H, L)
     j = encoder_block(j, p, pre + "joint_representation_encoder.", H, L)
+    _tap(taps, "enc.visual_encoder", v, True)
+    _tap(taps, "enc.physiological_encoder", a, True)
+    _tap(taps, "enc.joint_representation_encoder", j, True)
     cv, cp, cpv = pre + "cross_attention_v.", pre + "cross_attention_p.", pre + "cross_attention_pv."
     outs = [mha(v, a, a, p, cv, H),                                             # :142-167
             mha(a, v, v, p, cp, H),
@@ -108,6 +191,8 @@ def w_jr_forward(visual, phys, p: P, pre: str, H: int, L: int, output_format: st
             mha(v, j, j, p, cv, H),
             mha(j, a, a, p, cpv, H),
             mha(a, j, j, p, cp, H)]
+    for i, o in enumerate(outs):
+        _tap(taps, f"ca.{i}", o, True)
     if output_format == "SELF_ATTEN":                                           # :169-199
         st = torch.stack(outs, dim=2)                     # (T, B, 6, E)
         st = st.permute(1, 0, 2, 3)                       # (B, T, 6, E)
@@ -121,15 +206,20 @@ def w_jr_forward(visual, phys, p: P, pre: str, H: int, L: int, output_format: st
     return linear(cat, p[pre + "out_layer1.weight"], p[pre + "out_layer1.bias"])
 
 
-def wo_jr_forward(visual, phys, p: P, pre: str, H: int, L: int):
+def wo_jr_forward(visual, phys, p: P, pre: str, H: int, L: int, taps=None):
     """MultimodalTransformer_wo_JR.forward (models/mm_transformers.py:119-146).  The encoders are
     applied to (B, T, D) directly, i.e. self-attention runs over the batch axis (:120-122)."""
     v = encoder_block(visual, p, pre + "visual_encoder.", H, L)
     a = encoder_block(phys, p, pre + "physiological_encoder.", H, L)
+    _tap(taps, "enc.visual_encoder", v, False)
+    _tap(taps, "enc.physiological_encoder", a, False)
     ov = mha(v.permute(1, 0, 2), a.permute(1, 0, 2), a.permute(1, 0, 2), p,
-             pre + "cross_attention_v.", H).permute(1, 0, 2)
+             pre + "cross_attention_v.", H)
     op = mha(a.permute(1, 0, 2), v.permute(1, 0, 2), v.permute(1, 0, 2), p,
-             pre + "cross_attention_p.", H).permute(1, 0, 2)
+             pre + "cross_attention_p.", H)
+    ov, op = ov.permute(1, 0, 2), op.permute(1, 0, 2)
+    _tap(taps, "ca.0", ov, False)
+    _tap(taps, "ca.1", op, False)
     return linear(torch.cat((ov, op), dim=2), p[pre + "final_layer.weight"],
                   p[pre + "final_layer.bias"])
 
@@ -158,25 +248,27 @@ def regressor(x, p: P, pre: str):
     """Linear(dim,128)-ReLU-Dropout(p)-Linear(128,1) (two_transformers.py:104-114); dropout is
     identity at p=0 (config_file.json:69-70) and in eval."""
     h = torch.relu(linear(x, p[pre + "0.weight"], p[pre + "0.bias"]))
-    return linear(h, p[pre + "3.weight"], p[pre + "3.bias"])
+    return linear(h, p[pre + "3.weight"], p[pre + "3.bias"], out_round=False)   # fp32 out
 
 
 def two_transformers_forward(audio, video, p: P, H: int, L: int, joint_modalities: str,
-                             output_format: str = "FC", vision_in_ft: int = 512):
+                             output_format: str = "FC", vision_in_ft: int = 512, taps=None):
     """Two_transformers.forward (models/two_transformers.py:116-128).  Argument order is
-    (f1_norm=audio, f2_norm=video)."""
+    (f1_norm=audio, f2_norm=video).  `taps` (optional dict) receives the intermediates the golden
+    generator records (encoder outputs, the cross-attention outputs, the regressors' input)."""
     vid = l2_normalize(video)
     aud = l2_normalize(audio)
     if vision_in_ft != 512:
         vid = linear(vid, p["linear.weight"], p["linear.bias"])
     if joint_modalities == "TRANSFORMER":
-        av = w_jr_forward(vid, aud, p, "mm_transformer.", H, L, output_format)
+        av = w_jr_forward(vid, aud, p, "mm_transformer.", H, L, output_format, taps)
     elif joint_modalities == "FC":
         av = feature_concat_fc(vid, aud, p, "mm_transformer.")
     elif joint_modalities == "NONE":
-        av = wo_jr_forward(vid, aud, p, "mm_transformer.", H, L)
+        av = wo_jr_forward(vid, aud, p, "mm_transformer.", H, L, taps)
     else:
         raise NotImplementedError(joint_modalities)
+    _tap(taps, "head", av, joint_modalities == "TRANSFORMER" and output_format == "FC")
     vo = regressor(av, p, "vregressor.")
     ao = regressor(av, p, "aregressor.")
     return vo.squeeze(2), ao.squeeze(2)

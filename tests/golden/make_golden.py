@@ -83,6 +83,55 @@ def checksum(x: np.ndarray) -> float:
     return float(np.float64(x).sum() + (np.float64(x) ** 2).sum())
 
 
+def tap_intermediates(model, c, taps):
+    """Forward hooks on the reference's own submodules: each encoder block's output, the six
+    cross-attention outputs in call order (mm_multi_transformers.py:142-167 /
+    mm_transformers.py:125-135) and the regressors' input (the fusion output); a tensor hook on
+    each records dL/d(that tensor).  Everything is stored canonically as (B, T, F) rows."""
+    mm = model.mm_transformer
+    handles = []
+
+    def add(name, seq_first):
+        def store(t):
+            taps[name] = {"val": (t.permute(1, 0, 2) if seq_first else t).detach().clone()}
+
+            def ghook(g):
+                taps[name]["grad"] = (g.permute(1, 0, 2) if seq_first else g).detach().clone()
+            t.register_hook(ghook)
+        return store
+
+    if c["jm"] in ("TRANSFORMER", "NONE"):
+        encs = ["visual_encoder", "physiological_encoder"]
+        if c["jm"] == "TRANSFORMER":
+            encs.append("joint_representation_encoder")
+        for e in encs:
+            st = add("enc." + e, c["jm"] == "TRANSFORMER")
+            handles.append(getattr(mm, e).register_forward_hook(
+                lambda mod, inp, o, st=st: st(o)))
+        calls = []
+        cas = ["cross_attention_v", "cross_attention_p"] + (
+            ["cross_attention_pv"] if c["jm"] == "TRANSFORMER" else [])
+        for ca in cas:
+            def h(mod, inp, o):
+                add(f"ca.{len(calls)}", True)(o[0])
+                calls.append(1)
+            handles.append(getattr(mm, ca).register_forward_hook(h))
+    head_sf = c["jm"] == "TRANSFORMER" and c["fmt"] == "FC"
+    st_head = add("head", head_sf)
+    handles.append(model.vregressor.register_forward_hook(lambda mod, inp, o: st_head(inp[0])))
+    return handles
+
+
+def record_intermediates(out: dict, tag: str, taps: dict, B: int, T: int):
+    idx = np.unique(np.linspace(0, B * T - 1, spec.N_INTER_ROWS).round().astype(np.int64))
+    out[f"{tag}/inter_rows"] = idx
+    for name, d in taps.items():
+        for kind in ("val", "grad"):
+            x = d[kind].reshape(B * T, -1).double()
+            out[f"{tag}/inter/{name}:{kind}_norm"] = np.array(float(x.norm()))
+            out[f"{tag}/inter/{name}:{kind}_rows"] = x[torch.from_numpy(idx)].float().numpy()
+
+
 def run_two_transformers(mods, out, c):
     tag = c["tag"]
     torch.manual_seed(0)
@@ -99,6 +148,8 @@ def run_two_transformers(mods, out, c):
     a = torch.from_numpy(audio).requires_grad_(True)
     v = torch.from_numpy(video).requires_grad_(True)
     crit = make_loss(mods, "CCCLoss", 1)
+    taps = {}
+    handles = tap_intermediates(model, c, taps) if c.get("inter") else []
     aud = fc(a)
     vo, ao = model(aud, v)
     out[f"{tag}/vouts"] = vo.detach().numpy()
@@ -112,6 +163,10 @@ def run_two_transformers(mods, out, c):
     out[f"{tag}/v_loss"] = np.array(float(l1))
     out[f"{tag}/a_loss"] = np.array(float(l2))
     (l1 + l2).backward()
+    for h in handles:
+        h.remove()
+    if taps:
+        record_intermediates(out, tag, taps, B, T)
     grad_record(out, tag, list(model.named_parameters()))
     grad_record(out, tag, [("fc." + n, p) for n, p in fc.named_parameters()])
     grad_record(out, tag, [("input.audio", a), ("input.video", v)])

@@ -7,14 +7,18 @@ import numpy as np
 from oracle import hashinit as hi
 
 N_SAMPLE = 64
+N_INTER_ROWS = 8      # (b, t) rows sampled from each recorded intermediate (make_golden.py)
 
 # Two_transformers (+ FcLayer(1024,512) on the audio, as main.py:379 / train.py:265) cases.
 TT_CASES = [
-    dict(tag="none_fc", jm="NONE", fmt="FC", H=1, L=1, B=2, T=37, vin=2048),
-    dict(tag="tr_fc", jm="TRANSFORMER", fmt="FC", H=1, L=1, B=2, T=37, vin=2048, train_steps=3),
+    dict(tag="none_fc", jm="NONE", fmt="FC", H=1, L=1, B=2, T=37, vin=2048, inter=True),
+    dict(tag="tr_fc", jm="TRANSFORMER", fmt="FC", H=1, L=1, B=2, T=37, vin=2048, train_steps=3,
+         inter=True),
     dict(tag="tr_fc_h8l2", jm="TRANSFORMER", fmt="FC", H=8, L=2, B=2, T=16, vin=2048),
-    dict(tag="tr_sa", jm="TRANSFORMER", fmt="SELF_ATTEN", H=1, L=1, B=2, T=16, vin=2048),
-    dict(tag="tr_fc_t300", jm="TRANSFORMER", fmt="FC", H=1, L=1, B=2, T=300, vin=2048),
+    dict(tag="tr_sa", jm="TRANSFORMER", fmt="SELF_ATTEN", H=1, L=1, B=2, T=16, vin=2048,
+         inter=True),
+    dict(tag="tr_fc_t300", jm="TRANSFORMER", fmt="FC", H=1, L=1, B=2, T=300, vin=2048,
+         inter=True),
     dict(tag="fcjoint", jm="FC", fmt="FC", H=1, L=1, B=3, T=37, vin=512),
 ]
 

@@ -16,7 +16,22 @@ def rel_err(a, b) -> float:
     return float(np.abs(a - b).max() / den)
 
 
-def oracle_tt(c: dict) -> dict:
+def canon(t, seq_first: bool):
+    """(T, B, F) -> (B, T, F) when seq_first (the goldens' canonical intermediate layout)."""
+    if t is None:
+        return None
+    return t.permute(1, 0, 2) if seq_first else t
+
+
+def oracle_tt(c: dict, emulate=None, loss_scale: float = 1.0) -> dict:
+    """The golden case through the oracle; `emulate` = 16-bit storage emulation dtype
+    (R.emulate_storage), `loss_scale` = GradScaler-style scaling of the backward (grads are
+    returned unscaled)."""
+    with R.emulate_storage(emulate):
+        return _oracle_tt(c, loss_scale)
+
+
+def _oracle_tt(c: dict, loss_scale: float) -> dict:
     tag = c["tag"]
     shapes = R.two_transformers_shapes(c["L"], c["jm"], c["fmt"], c["vin"])
     p = R.hash_params(shapes, "")
@@ -28,18 +43,25 @@ def oracle_tt(c: dict) -> dict:
     a = torch.from_numpy(audio).requires_grad_(True)
     v = torch.from_numpy(video).requires_grad_(True)
     aud = R.linear(a, fcp["fc_layer.weight"], fcp["fc_layer.bias"])
-    vo, ao = R.two_transformers_forward(aud, v, p, c["H"], c["L"], c["jm"], c["fmt"], c["vin"])
+    taps = {}
+    vo, ao = R.two_transformers_forward(aud, v, p, c["H"], c["L"], c["jm"], c["fmt"], c["vin"],
+                                        taps=taps)
+    for t, _ in taps.values():
+        t.retain_grad()
     l1 = R.ccc_loss(vo.reshape(1, -1), torch.from_numpy(lv).reshape(1, -1))
     l2 = R.ccc_loss(ao.reshape(1, -1), torch.from_numpy(la).reshape(1, -1))
-    (l1 + l2).backward()
+    ((l1 + l2) * loss_scale).backward()
+    uns = lambda g: None if g is None else g / loss_scale
     res = {"vouts": vo.detach().numpy(), "aouts": ao.detach().numpy(),
-           "v_loss": float(l1), "a_loss": float(l2), "grads": {}}
+           "v_loss": float(l1), "a_loss": float(l2), "grads": {},
+           "taps": {k: {"val": canon(t.detach(), sf), "grad": uns(canon(t.grad, sf))}
+                    for k, (t, sf) in taps.items()}}
     for k, t in p.items():
-        res["grads"][k] = t.grad
+        res["grads"][k] = uns(t.grad)
     for k, t in fcp.items():
-        res["grads"]["fc." + k] = t.grad
-    res["grads"]["input.audio"] = a.grad
-    res["grads"]["input.video"] = v.grad
+        res["grads"]["fc." + k] = uns(t.grad)
+    res["grads"]["input.audio"] = uns(a.grad)
+    res["grads"]["input.video"] = uns(v.grad)
     return res
 
 
@@ -73,7 +95,33 @@ def compare_grads(golden: dict, tag: str, grads: dict, tol: float):
     return bad
 
 
-def oracle_intra(c: dict) -> dict:
+def inter_errors(golden: dict, tag: str, taps: dict):
+    """Relative Frobenius error of the recorded intermediates (and of their gradients) on the
+    golden's sampled (b, t) rows: {name:kind: err}.  taps[name] = {"val": (B,T,F), "grad": ...}
+    (canonical layout, any device / dtype).  Every golden intermediate must be present."""
+    idx = torch.from_numpy(golden[tag + "/inter_rows"])
+    names = sorted({k.split("/inter/")[1].split(":")[0] for k in golden
+                    if k.startswith(tag + "/inter/")})
+    errs = {}
+    for name in names:
+        for kind in ("val", "grad"):
+            ref = golden[f"{tag}/inter/{name}:{kind}_rows"].astype(np.float64)
+            t = taps.get(name, {}).get(kind)
+            if t is None:
+                errs[f"{name}:{kind}"] = float("inf")
+                continue
+            got = t.detach().double().cpu().reshape(-1, ref.shape[1])[idx].numpy()
+            errs[f"{name}:{kind}"] = float(np.linalg.norm(got - ref) /
+                                           max(np.linalg.norm(ref), 1e-30))
+    return errs
+
+
+def oracle_intra(c: dict, emulate=None) -> dict:
+    with R.emulate_storage(emulate):
+        return _oracle_intra(c)
+
+
+def _oracle_intra(c: dict) -> dict:
     tag = c["tag"]
     p = R.hash_params(R.intra_modal_shapes(512, c["L"]), "intra.")
     for t in p.values():

@@ -57,3 +57,19 @@ def test_missing_first_clip_raises(tmp_path):
         fs.window_rows("wavlm", [[("vidB", 1)]])
     with pytest.raises(KeyError):
         FR.window_feats(root, [[("vidB", 1)]], {}, DIM)
+
+
+def test_default_store_is_fp32_exact(tmp_path):
+    """The reference loads the wavLM features as fp32 np.load values (train.py:157-158): the
+    default store keeps them bit-exact (fp16 storage is an explicit opt-in)."""
+    root = str(tmp_path / "npy")
+    lengths = make_tree(root)
+    store_dir = str(tmp_path / "store")
+    FeatureStoreWriter.from_npy_tree(store_dir, root, "wavlm", DIM, lengths=lengths)
+    fs = FeatureStore(store_dir, device="cpu")
+    table = fs.tables["wavlm"]
+    assert table.dtype.is_floating_point and table.element_size() == 4
+    rows, _ = fs.window_rows("wavlm", [[("vidA", k) for k in (1, 2, 3)]])
+    for j, k in enumerate((1, 2, 3)):
+        ref = np.load(os.path.join(root, "vidA", f"{k}.npy"))
+        np.testing.assert_array_equal(table[int(rows[0, j]), :DIM].numpy(), ref)

@@ -1,0 +1,129 @@
+"""Parity at the BASELINE.json configs' own shapes, HIP drop-ins vs the CPU
+oracle (oracle/jmt_ref.py, pinned by the reference goldens):
+
+* c3 at the bench shape (B=64, T=300, D_a=1024, D_v=2048, bf16, torch default init as bench.py):
+  the fusion forward is window-independent in TRANSFORMER mode (attention runs over T inside a
+  window), so a subset of the 64 windows is checked against the fp32 oracle (north_star: 1e-2
+  bf16), and the full-batch CCC losses against the oracle's CCC of the GPU predictions;
+* c4 long window (T=1024) and c2 (NONE/FC: wo_JR self-attention over the batch axis, Lq = B =
+  32 over 300 "batches") at their real sequence shapes, fp32 (1e-4) and bf16 (error model of
+  tests/parity.py), with the discriminative hash-init weights."""
+import numpy as np
+import pytest
+import torch
+
+from jmt import functional as JF
+from oracle import jmt_ref as R
+from oracle.hashinit import init_module_
+from tests.parity import K16, UNIT
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+E = 512
+
+
+def _models(jm, vin, T, hashed: bool, seed=0):
+    from models.two_transformers import Two_transformers
+    from models.fc_layer import FcLayer
+    torch.manual_seed(seed)
+    m = Two_transformers(0.0, 0.0, 1, 1, jm, "FC", vin)
+    fc = FcLayer(1024, E)
+    if hashed:
+        init_module_(m, "")
+        init_module_(fc, "fc.")
+    return m.to(DEV), fc.to(DEV)
+
+
+def _state(m, fc):
+    p = {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
+    fp = {k: v.detach().float().cpu() for k, v in fc.state_dict().items()}
+    return p, fp
+
+
+def _oracle_fwd(p, fp, audio, video, jm, vin):
+    with torch.no_grad():
+        aud = R.linear(audio, fp["fc_layer.weight"], fp["fc_layer.bias"])
+        return R.two_transformers_forward(aud, video, p, 1, 1, jm, "FC", vin)
+
+
+def test_c3_bench_shape_window_subset_bf16():
+    from losses.loss import CCCLoss
+    torch.set_num_threads(16)
+    B, T = 64, 300
+    m, fc = _models("TRANSFORMER", 2048, T, hashed=False)
+    g = torch.Generator(device=DEV).manual_seed(1000)
+    audio = torch.randn(B, T, 1024, device=DEV, generator=g)
+    video = torch.randn(B, T, 2048, device=DEV, generator=g)
+    lv = (torch.rand(B, T, device=DEV, generator=g) * 2 - 1).view(-1, B * T)
+    la = (torch.rand(B, T, device=DEV, generator=g) * 2 - 1).view(-1, B * T)
+    crit = CCCLoss(1)
+    with JF.compute_mode(torch.bfloat16):
+        vo, ao = m(fc(audio), video)                         # (T, B) seq-first, as the reference
+        l1 = crit(vo.view(-1, B * T), lv)
+        l2 = crit(ao.view(-1, B * T), la)
+        (l1 + l2).backward()
+    torch.cuda.synchronize()
+    p, fp = _state(m, fc)
+    win = [0, 21, 42, 63]
+    rvo, rao = _oracle_fwd(p, fp, audio[win].cpu(), video[win].cpu(), "TRANSFORMER", 2048)
+    for got, ref in ((vo[:, win], rvo), (ao[:, win], rao)):
+        err = float((got.float().cpu() - ref).abs().max())
+        assert err <= 1e-2, err                              # north_star bf16 bound
+    # full-batch losses: the GPU CCC of the GPU predictions == the oracle CCC of them (fp32)
+    rl1 = float(R.ccc_loss(vo.detach().float().cpu().reshape(1, -1), lv.cpu()))
+    rl2 = float(R.ccc_loss(ao.detach().float().cpu().reshape(1, -1), la.cpu()))
+    assert abs(float(l1) - rl1) <= 1e-5 and abs(float(l2) - rl2) <= 1e-5, (float(l1), rl1)
+    gw = m.mm_transformer.out_layer1.weight.grad
+    assert gw is not None and bool(torch.isfinite(gw).all()) and float(gw.abs().max()) > 0
+
+
+def _run_gpu(m, fc, audio, video, lv, la, cd):
+    from losses.loss import CCCLoss
+    crit = CCCLoss(1)
+    B, T = lv.shape
+    with JF.compute_mode(cd):
+        vo, ao = m(fc(audio.to(DEV)), video.to(DEV))
+        l1 = crit(vo.reshape(-1, B * T), lv.to(DEV).view(-1, B * T))
+        l2 = crit(ao.reshape(-1, B * T), la.to(DEV).view(-1, B * T))
+        (l1 + l2).backward()
+    return vo.detach().float().cpu(), ao.detach().float().cpu(), float(l1 + l2)
+
+
+def _oracle_loss(p, fp, audio, video, lv, la, jm, vin):
+    vo, ao = _oracle_fwd(p, fp, audio, video, jm, vin)
+    B, T = lv.shape
+    loss = R.ccc_loss(vo.reshape(1, -1), lv.reshape(1, -1)) + \
+        R.ccc_loss(ao.reshape(1, -1), la.reshape(1, -1))
+    return vo, ao, float(loss)
+
+
+@pytest.mark.parametrize("cfg", [("c4", "TRANSFORMER", 2, 1024), ("c2", "NONE", 32, 300)],
+                         ids=["c4_T1024", "c2_B32_T300"])
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+def test_config_shapes_vs_oracle(cfg, cd):
+    from oracle.hashinit import features, labels
+    torch.set_num_threads(16)
+    name, jm, B, T = cfg
+    m, fc = _models(jm, 2048, T, hashed=True)
+    audio = torch.from_numpy(features(name + ".audio", (B, T, 1024)))
+    video = torch.from_numpy(features(name + ".video", (B, T, 2048)))
+    lv = torch.from_numpy(labels(name + ".lv", (B, T)))
+    la = torch.from_numpy(labels(name + ".la", (B, T)))
+    vo, ao, loss = _run_gpu(m, fc, audio, video, lv, la, cd)
+    p, fp = _state(m, fc)
+    rvo, rao, rloss = _oracle_loss(p, fp, audio, video, lv, la, jm, 2048)
+    assert vo.shape == rvo.shape
+    spread = float(max(rvo.max() - rvo.min(), rao.max() - rao.min()))
+    assert spread > 0.1, spread                                # the check carries signal
+    if cd == torch.float32:
+        for got, ref in ((vo, rvo), (ao, rao)):
+            assert float((got - ref).abs().max()) <= 1e-4 * max(1.0, float(ref.abs().max()))
+        assert abs(loss - rloss) <= 1e-4
+        return
+    with R.emulate_storage(cd):
+        evo, eao, eloss = _oracle_loss(p, fp, audio, video, lv, la, jm, 2048)
+    for got, emu, ref in ((vo, evo, rvo), (ao, eao, rao)):
+        e_gpu = float((got - ref).abs().max())
+        e_emu = float((emu - ref).abs().max())
+        assert e_gpu <= K16 * max(e_emu, UNIT[cd] * spread), (e_gpu, e_emu)
+    assert abs(loss - rloss) <= K16 * max(abs(eloss - rloss), UNIT[cd]), (loss, rloss, eloss)
