@@ -73,97 +73,154 @@ def step_flops(B: int, T: int, Da: int = D_A, Dv: int = D_V, fc: bool = True,
     return (3 * F - leaf) * B
 
 
-class GemmProbe:
-    """HIP-event timing of the dominant GEMM family over eager probe steps.  Each matching
-    launch of the step runs as usual; when it is idempotent (beta = 0, output aliasing no
-    input) it is then re-issued `reps` times back-to-back between ONE event pair on the
-    stream it is launched on (torch's current stream).  A pair around every single launch
-    reads 3-8 % above the kernel's rocprofv3 duration (the dispatch of the kernel after the
-    start marker is inside the pair: profiles/r01_event_check.txt); bracketing `reps`
-    launches spreads that over all of them."""
+class FamilyProbe:
+    """In-step timing of the step's kernel families over eager probe steps (right after the
+    timed region, same data and weights): one HIP event pair around EVERY launch of a family
+    (GEMM NT / NN / TN by operand majorness, fused attention forward / backward), recorded on
+    the stream the launch goes to (torch's current stream: the grouped path launches everything
+    there).  An event pair reads above the kernel's own duration (the dispatch after the start
+    marker and the end-of-kernel flush fall inside it: profiles/r01_event_check.txt), so each
+    launch is followed by two calibration pairs around empty launches (jmt_noop): one around a
+    single empty launch, one around two back to back.  overhead = pair(1) - (pair(2) - pair(1))
+    (the pair's fixed cost without the empty kernel's own execution) is subtracted from every
+    launch's reading."""
 
-    def __init__(self, key, reps: int = 8):
-        self.key = key
-        self.reps = reps
+    def __init__(self):
         self.on = False
-        self.events = []
-        self.flops = []
-        self.bytes = []
+        self.rec = []
+        self.cal = []
 
-    def __call__(self, info, launch):
-        if not self.on or (info["ab_dtype"], info["a_kmajor"], info["b_kmajor"]) != self.key:
-            return launch()
-        s1 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        s1.record()
-        r = launch()
-        e1.record()
-        if info.get("beta", 0.0) != 0.0 or info.get("inplace", False):
-            return r
+    @staticmethod
+    def _pair(fn):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
-        for _ in range(self.reps):
-            launch()
+        r = fn()
         e.record()
-        self.events.append((s, e, s1, e1))
-        self.flops.append(2.0 * info["M"] * info["N"] * info["K"] * info["batch"])
-        ab = 4 if info["ab_dtype"] == 0 else 2
-        cb = 4 if info["c_dtype"] == 0 else 2
-        self.bytes.append(info["batch"] * ((info["M"] + info["N"]) * info["K"] * ab +
-                                           info["M"] * info["N"] * cb))
+        return r, (s, e)
+
+    def __call__(self, info, launch):
+        if not self.on:
+            return launch()
+        from jmt import ops
+        r, ev = self._pair(launch)
+        self.rec.append((info["family"], info["flops"], info.get("bytes"), ev))
+        _, e1 = self._pair(ops.noop)
+        _, e2 = self._pair(lambda: (ops.noop(), ops.noop()))
+        self.cal.append((e1, e2))
         return r
 
-    def summary(self):
-        if not self.events:
+    def summary(self, probe_steps: int):
+        if not self.rec:
             return None
-        ms = [s.elapsed_time(e) / self.reps for s, e, _, _ in self.events]
-        ms1 = [s1.elapsed_time(e1) for _, _, s1, e1 in self.events]
-        return {"launches": len(ms), "avg_ms": sum(ms) / len(ms),
-                "avg_ms_single_pair": sum(ms1) / len(ms1),
-                "avg_flops": sum(self.flops) / len(self.flops),
-                "avg_bytes": sum(self.bytes) / len(self.bytes),
-                "total_ms": sum(ms)}
+        import statistics
+        ms = lambda ev: ev[0].elapsed_time(ev[1])
+        one = statistics.median(ms(a) for a, _ in self.cal)
+        two = statistics.median(ms(b) for _, b in self.cal)
+        over = max(0.0, one - (two - one))
+        fam = {}
+        for f, fl, by, ev in self.rec:
+            d = fam.setdefault(f, {"launches": 0, "ms": 0.0, "ms_raw": 0.0, "flops": 0.0,
+                                   "bytes": 0.0})
+            d["launches"] += 1
+            d["ms_raw"] += ms(ev)
+            d["ms"] += max(ms(ev) - over, 1e-6)
+            d["flops"] += fl
+            d["bytes"] += by or 0.0
+        out = []
+        for f, d in fam.items():
+            tf = d["flops"] / (d["ms"] * 1e-3) / 1e12
+            out.append({"family": f, "launches_per_step": d["launches"] / probe_steps,
+                        "ms_per_step": round(d["ms"] / probe_steps, 4),
+                        "avg_launch_us": round(d["ms"] / d["launches"] * 1e3, 2),
+                        "avg_launch_us_raw": round(d["ms_raw"] / d["launches"] * 1e3, 2),
+                        "gflop_per_launch": round(d["flops"] / d["launches"] / 1e9, 3),
+                        "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
+                        "tflops": round(tf, 1), "frac": round(tf / PEAK_BF16_TFLOPS, 4)})
+        out.sort(key=lambda r: -r["ms_per_step"])
+        return {"families": out, "event_pair_overhead_us": round(over * 1e3, 2)}
 
 
-def cpu_baseline(model_sd, fc_sd, B, T, steps=2):
-    """The oracle (CPU restatement, oracle/jmt_ref.py) timed on this host: fp32 torch-CPU
-    forward+backward+SGD of the same step on a bounded sample (B windows, 1 warm-up)."""
+def parity_check(model, fc, audio, video, lv, la, cd, jm, fmt, Dv, nwin=2):
+    """BASELINE.json's '+ CCC parity': the GPU predictions and CCC losses in the compute dtype
+    vs the CPU oracle (oracle/jmt_ref.py, fp32, pinned by the reference goldens) on the first
+    `nwin` windows of the bench batch with the trained weights (north_star: 1e-2 bf16)."""
     from oracle import jmt_ref as R
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(16, ncpu))
+    from jmt import functional as JF
+    from losses.loss import CCCLoss
+    crit = CCCLoss(1)
+    a, v = audio[:nwin], video[:nwin]
+    T = a.shape[1]
+    yv = lv.view(audio.shape[0], T)[:nwin]
+    ya = la.view(audio.shape[0], T)[:nwin]
+    with torch.no_grad(), JF.compute_mode(cd):
+        vo, ao = model(fc(a) if fc is not None else a, v)
+        gl1 = float(crit(vo.reshape(1, -1), yv.reshape(1, -1)))
+        gl2 = float(crit(ao.reshape(1, -1), ya.reshape(1, -1)))
+    p = {k: t.detach().float().cpu() for k, t in model.state_dict().items()}
+    with torch.no_grad():
+        ac = a.float().cpu()
+        if fc is not None:
+            fp = {k: t.detach().float().cpu() for k, t in fc.state_dict().items()}
+            ac = R.linear(ac, fp["fc_layer.weight"], fp["fc_layer.bias"])
+        rvo, rao = R.two_transformers_forward(ac, v.float().cpu(), p, 1, 1, jm, fmt, Dv)
+        rl1 = float(R.ccc_loss(rvo.reshape(1, -1), yv.cpu().reshape(1, -1)))
+        rl2 = float(R.ccc_loss(rao.reshape(1, -1), ya.cpu().reshape(1, -1)))
+    err = max(float((vo.float().cpu() - rvo).abs().max()), float((ao.float().cpu() - rao).abs().max()))
+    lerr = max(abs(gl1 - rl1), abs(gl2 - rl2))
+    return {"reference": "oracle/jmt_ref.py fp32 CPU, same weights (after the timed steps) and "
+                         f"windows 0..{nwin - 1} of the bench batch",
+            "pred_max_abs_err": float(f"{err:.3g}"), "loss_max_abs_err": float(f"{lerr:.3g}"),
+            "pred_abs_max": float(f"{float(max(rvo.abs().max(), rao.abs().max())):.3g}"),
+            "tolerance": 1e-2, "pass": bool(err <= 1e-2 and lerr <= 1e-2)}
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS, 16 per GPU on the
+    GPU pool, whose nproc shows the whole machine) or the affinity set."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    env = os.environ.get("OMP_NUM_THREADS")
+    return (max(1, min(int(env), aff)) if env and env.isdigit() else aff), aff
+
+
+def cpu_baseline(model_sd, fc_sd, audio, video, lv, la, steps=2):
+    """The oracle (CPU restatement, oracle/jmt_ref.py) timed on this host: fp32 torch-CPU
+    forward+backward+SGD of the SAME training step (rank 0's batch, the initial weights),
+    1 warm-up + `steps` timed steps."""
+    from oracle import jmt_ref as R
+    threads, aff = cpu_threads()
     torch.set_num_threads(threads)
-    g = torch.Generator().manual_seed(1234)
-    audio = torch.randn(B, T, D_A, generator=g)
-    video = torch.randn(B, T, D_V, generator=g)
-    lv = torch.rand(B, T, generator=g) * 2 - 1
-    la = torch.rand(B, T, generator=g) * 2 - 1
-    p = {k: v.detach().float().cpu().clone() for k, v in model_sd.items()}
-    fp = {k: v.detach().float().cpu().clone() for k, v in fc_sd.items()}
+    B, T = audio.shape[0], audio.shape[1]
+    a, v = audio.float().cpu(), video.float().cpu()
+    yv, ya = lv.float().cpu().view(B, T), la.float().cpu().view(B, T)
+    p = {k: t.detach().float().cpu().clone() for k, t in model_sd.items()}
+    fp = {k: t.detach().float().cpu().clone() for k, t in fc_sd.items()}
     bufs = {}
     times = []
     for i in range(steps + 1):
         t0 = time.perf_counter()
-        R.train_step(p, fp, audio, video, lv, la, 1, 1, "TRANSFORMER", "FC", 2048, bufs)
+        R.train_step(p, fp, a, v, yv, ya, 1, 1, "TRANSFORMER", "FC", v.shape[-1], bufs)
         times.append(time.perf_counter() - t0)
     t = sum(times[1:]) / steps
     return {"value": round(B / t, 3), "unit": "windows/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/jmt_ref.py train_step, B={B} T={T} fp32 torch-CPU, 1 warm-up + "
-                      f"{steps} timed steps ({t * 1e3:.0f} ms/step)"}
+            "sample": f"oracle/jmt_ref.py train_step on the bench batch (B={B} T={T}, rank 0's "
+                      f"data, initial weights), fp32 torch-CPU, {threads} threads (affinity set "
+                      f"{aff} CPUs; OMP_NUM_THREADS = the box's share), 1 warm-up + {steps} timed "
+                      f"steps ({t * 1e3:.0f} ms/step)"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
                     help="workload (c3 = the one BASELINE.json's metric is quoted on)")
     ap.add_argument("--batch", type=int, default=None, help="windows per GPU (config default)")
     ap.add_argument("--seq", type=int, default=None, help="T (config default)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=64)
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="no per-launch events (profiling)")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="replay the whole step as one hipGraph (default)")
@@ -254,7 +311,7 @@ def main():
             opt.step()
         return loss
 
-    probe = GemmProbe((ops.dt(cd), True, True))
+    probe = FamilyProbe()
     for _ in range(args.warmup):
         loss = step()
     torch.cuda.synchronize()
@@ -275,7 +332,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    probe.on = False
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = run()
@@ -284,7 +340,6 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    probe.on = False
     last_loss = float(loss.detach())
     if not args.no_probe:
         # per-launch HIP events cannot sit inside the replayed graph (and would add host work to
@@ -305,29 +360,29 @@ def main():
     windows = B * world * args.steps
     value = windows / elapsed
 
-    psum = probe.summary()
+    psum = probe.summary(args.probe_steps)
     roofline = None
-    # HBM bytes per launch of the same kernel family from the committed PMC passes
-    # (scripts/pmc_bench.sh: FETCH_SIZE / WRITE_SIZE, separate rocprofv3 passes, gfx950 correction)
-    traffic, traffic_src = None, None
-    tpath = os.path.join(REPO, "profiles", "r01_pmc_bench", "traffic_nt_gemm.json")
-    if args.config == "c3" and cd == torch.bfloat16 and os.path.exists(tpath):
-        traffic = round(json.load(open(tpath))["hbm_bytes_per_launch"])
-        traffic_src = os.path.relpath(tpath, REPO)
     if psum:
-        achieved = psum["avg_flops"] / (psum["avg_ms"] * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "kernel": f"gemm_kernel<{args.dtype},Kmajor,Kmajor> (NT: every forward "
-                    "linear: grouped in/out projections, FFN, FC head, regressors)", "achieved": round(achieved, 1),
-                    "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                    "traffic_unit": "HBM bytes per launch (PMC)",
+        dom = psum["families"][0]                  # the family with the most in-step time
+        # HBM bytes per launch of that family from the committed PMC passes
+        # (scripts/pmc_bench.sh: FETCH_SIZE / WRITE_SIZE, separate rocprofv3 passes, gfx950
+        # FETCH_SIZE x2 correction), when one exists for this workload
+        traffic, traffic_src = None, None
+        tpath = os.path.join(REPO, "profiles", "r02_pmc_bench", f"traffic_{dom['family']}.json")
+        if args.config == "c3" and cd == torch.bfloat16 and os.path.exists(tpath):
+            traffic = round(json.load(open(tpath))["hbm_bytes_per_launch"])
+            traffic_src = os.path.relpath(tpath, REPO)
+        roofline = {"bound": "mfma", "kernel": dom["family"], "achieved": dom["tflops"],
+                    "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": dom["frac"],
+                    "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
                     "traffic_source": traffic_src,
-                    "algorithmic_bytes_per_launch": round(psum["avg_bytes"]),
-                    "launches_per_step": psum["launches"] // args.probe_steps,
-                    "timed_over": f"eager probe steps after the timed region; each launch re-issued {probe.reps}x between one event pair",
-                    "avg_launch_us": round(psum["avg_ms"] * 1e3, 2),
-                    "avg_launch_us_single_pair": round(psum["avg_ms_single_pair"] * 1e3, 2),
-                    "avg_gflop_per_launch": round(psum["avg_flops"] / 1e9, 3)}
+                    "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"] or None,
+                    "avg_launch_us": dom["avg_launch_us"],
+                    "launches_per_step": dom["launches_per_step"],
+                    "timed_over": f"{args.probe_steps} eager probe steps after the timed region, "
+                                  "one event pair per launch minus the empty-launch pair "
+                                  f"overhead ({psum['event_pair_overhead_us']} us)",
+                    "families": psum["families"]}
     sfl = step_flops(B, T, **fl_kw)
     step_mfma = None
     if sfl is not None:
@@ -336,9 +391,12 @@ def main():
                      "achieved_tflops": round(step_tf, 1),
                      "frac_of_peak": round(step_tf / (PEAK_BF16_TFLOPS * world), 4)}
 
+    parity = None
+    if rank == 0 and not args.no_parity:
+        parity = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
-        cpu = cpu_baseline(model_sd0, fc_sd0, args.cpu_batch, T)
+        cpu = cpu_baseline(model_sd0, fc_sd0, audio, video, lv, la)
 
     if rank == 0:
         out = {
@@ -354,6 +412,7 @@ def main():
                        "loss_scaling": "device GradScaler" if scaler is not None else None},
             "roofline": roofline,
             "step_mfma": step_mfma,
+            "parity": parity,
             "cpu_baseline": cpu,
             "final_loss": round(last_loss, 6),
             "graph": bool(use_graph),

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define JMT_ABI_VERSION 2
+#define JMT_ABI_VERSION 3
 
 enum { JMT_F32 = 0, JMT_BF16 = 1, JMT_F16 = 2 };
 enum { JMT_OK = 0, JMT_ERR_ARG = -1, JMT_ERR_HIP = -2, JMT_ERR_UNSUPPORTED = -3 };
@@ -135,23 +135,24 @@ int jmt_softmax_bwd(int p_dt, int ds_dt, int64_t rows, int n, const void* p, int
  * dh = 512); otherwise the entry points return JMT_ERR_UNSUPPORTED and the caller uses the
  * GEMM + jmt_softmax path.
  * jmt_attn_fwd: writes o and, if lse != NULL, lse[(n*H + h)*Lq + l] = ln sum_k exp(scale s_lk).
- *   Training: p_out != NULL receives the UNNORMALISED probabilities (N*H*Lq rows of ldp, columns
- *   [Lk, ldp) zero) and mt (jmt_attn_mt_floats floats) each key tile's reference max;
- *   jmt_attn_bwd_dq normalises them in place.
- * jmt_attn_bwd_dq: given dO (go), o, k, v, lse and the forward's p / mt: rewrites p as the exact
- *   probabilities, writes ds = scale * P o (dO V^T - rowsum(dO o O)) (same layout as p) and
- *   dq = ds K.  dK = ds^T Q and dV = P^T dO are left to jmt_gemm. */
+ *   No probabilities are kept: the backward recomputes them from lse.
+ * jmt_attn_bwd: given dO (go), the forward's o and lse, and q, k, v: recomputes
+ *   P = exp(scale Q K^T - lse), writes p_out = P and ds_out = scale * P o (dO V^T - rowsum(dO o O))
+ *   (N*H*Lq rows of ldp >= Lk, row (n*H + h)*Lq + l; columns [Lk, ldp) zero) and
+ *   dq = ds K.  dK = ds^T Q and dV = P^T dO are left to jmt_gemm.
+ * (ABI 3: replaces ABI 2's jmt_attn_fwd p_out/mt outputs, jmt_attn_mt_floats and
+ * jmt_attn_bwd_dq.) */
 int jmt_attn_supported(int dt, int dh);
-int jmt_attn_mt_floats(int N, int H, int Lq, int Lk);
 int jmt_attn_fwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* q, int64_t sq_l,
                  int64_t sq_n, const void* k, int64_t sk_l, int64_t sk_n, const void* v,
                  int64_t sv_l, int64_t sv_n, void* o, int64_t so_l, int64_t so_n, float scale,
-                 float* lse, void* p_out, int64_t ldp, float* mt, void* stream);
-int jmt_attn_bwd_dq(int dt, int N, int H, int Lq, int Lk, int dh, const void* go, int64_t sgo_l,
-                    int64_t sgo_n, const void* o, int64_t so_l, int64_t so_n, const void* k,
-                    int64_t sk_l, int64_t sk_n, const void* v, int64_t sv_l, int64_t sv_n,
-                    const float* lse, void* p, const float* mt, int64_t ldp, void* ds, void* dq,
-                    int64_t sdq_l, int64_t sdq_n, float scale, void* stream);
+                 float* lse, void* stream);
+int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* go, int64_t sgo_l,
+                 int64_t sgo_n, const void* o, int64_t so_l, int64_t so_n, const void* q,
+                 int64_t sq_l, int64_t sq_n, const void* k, int64_t sk_l, int64_t sk_n,
+                 const void* v, int64_t sv_l, int64_t sv_n, const float* lse, void* p_out,
+                 void* ds_out, int64_t ldp, void* dq, int64_t sdq_l, int64_t sdq_n, float scale,
+                 void* stream);
 
 /* Bias gradient: db[n] (+)= sum_m dy[m][n] (two-phase, deterministic, fp32 partial slabs of
  * jmt_colsum_blocks(rows) * N floats). */
@@ -168,6 +169,9 @@ int jmt_colsum_grouped(int dt, int G, int64_t rows, int N, const void* dy, int64
 /* Strided 2-D copy with dtype conversion and optional transpose (layout plumbing:
  * the (T,B) output of the FC head, torch.stack of the SELF_ATTEN head). dst may be accumulated
  * into (accumulate=1). */
+/* An empty one-block launch (measurement: the overhead of an event pair around a launch). */
+int jmt_noop(void* stream);
+
 int jmt_copy2d(int src_dt, int dst_dt, int64_t rows, int64_t cols, const void* src,
                int64_t src_rs, int64_t src_cs, void* dst, int64_t dst_rs, int64_t dst_cs,
                int accumulate, void* stream);

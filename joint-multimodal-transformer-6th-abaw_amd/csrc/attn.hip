@@ -1,345 +1,547 @@
-// Fused scaled-dot-product attention for the JMT path (gfx950, wave64), forward and the dQ half
-// of the backward, per (batch n, head h):
-//   forward:  O = softmax(scale Q K^T) V,  + lse and (training) the probabilities P
-//   backward: dP = dO V^T,  dS = scale * P o (dP - rowsum(dO o O)),  dQ = dS K   (+ P, dS out)
+// Fused scaled-dot-product attention for the JMT path (gfx950, wave64), head_dim 512, per
+// (batch n, head h):
+//   forward:  O = softmax(scale Q K^T) V, + lse (natural log of the row sums, scaled scores)
+//   backward: P = exp(scale Q K^T - lse) recomputed, dP = dO V^T, Delta = rowsum(dO o O),
+//             dS = scale P o (dP - Delta), dQ = dS K;  P and dS written once (bf16/f16) for the
+//             dK = dS^T Q / dV = P^T dO GEMMs
 // Replaces the score GEMM -> softmax -> PV GEMM chain behind every nn.MultiheadAttention of the
 // reference (F.multi_head_attention_forward, called from mm_multi_transformers.py:57,142-167,
-// 191 and intra_modal_transformer_fusion.py) and the dP GEMM + softmax
-// backward + dQ GEMM of its autograd backward; dK = dS^T Q and dV = P^T dO stay GEMMs.
+// 191 and intra_modal_transformer_fusion.py) and its autograd backward.
 //
-// Both passes are the same kernel shape (MODE): a block of 4 waves owns 64 rows of the "row
-// operand" (Q forward, dO backward); wave w owns rows 16w..16w+15: their fragments stay in
-// registers, a 16 x DH fp32 accumulator (O / dQ) in registers.  Key tiles of 64 stream through
-// two LDS images: the SCORE stream (K forward, V backward) is read as ds_read_b128 fragments for
-// the 16x64 score tile, the ACCUMULATE stream (V forward, K backward) through
-// ds_read_b64_tr_b16 for the 16 x DH update.  Stream 2 of tile j lands during the score phase,
-// stream 1 of tile j+1 during the update phase.
+// Geometry (both kernels): a block is 8 waves (512 threads, 2 waves per SIMD at one block per
+// CU) owning 64 rows of the row operand (Q forward, Q / dO backward).  Wave w owns rows
+// 16 (w & 3) .. +15 and HALF h = w >> 2 of the 512 head dims: its row-operand fragments
+// (16 rows x 256 dims) and its accumulator (O or dQ: 16 rows x 256 dims, 64 registers) stay in
+// registers.  The contraction over head dims of the score products (Q K^T, dO V^T) is split
+// between the two waves of a pair (w, w ^ 4): each writes its 16 x KT fp32 partial into an LDS
+// exchange slot, the pair adds them in one canonical order (half 0 + half 1, so both hold
+// bitwise the same scores), and both run the same softmax; the update products (P V, dS K)
+// need no exchange: each wave produces its own 256 output dims.  This halves the registers of
+// the round-1 kernel (453 VGPRs, one wave per SIMD) so two waves per SIMD hide LDS / MFMA
+// latency.
 //
-//  * Both products run with the MFMA operands swapped (stream operand first), so an accumulator
-//    lane owns ONE row and 4 consecutive keys / head columns: softmax row state is lane-local
-//    (2 shuffles per row reduction), the probabilities (or dS) feed the update MFMA straight from
-//    registers (their k-slot order is mirrored in the transposed fragment reads), and output
-//    rows are stored as 8-B column groups.
-//  * Forward softmax is online with LAZY rescaling: probabilities are taken against a reference
-//    max that is raised (O and the row sum rescaled) only when a row max exceeds it by > 8
-//    (log2 units).  With P output on, the unnormalised tile values and each tile's reference max
-//    are written; the backward kernel normalises them with the lse and writes the exact P back
-//    for the dV GEMM.
-//  * Images: [key][DH] rows at a 32-B padded pitch (AttnGeo) -> conflict-free fragment reads with
-//    immediate offsets.  XCD-aware block order: the q-tile blocks of one (n, h) share an L2.
+//  * MFMA operands swapped (stream operand first): an accumulator lane owns ONE row and 4
+//    consecutive keys / dims, softmax row state is lane-local (2 shuffles per row reduction),
+//    probabilities (or dS) feed the update MFMA straight from registers (their k-slot order is
+//    mirrored in the transposed fragment reads of the stream image).
+//  * K / V images: [rows][1024 B] with no padding, 16-B chunk c of row r stored at chunk
+//    c ^ ((r & 7) << 1): the ds_read_b128 score fragments and the ds_read_b64_tr_b16 update
+//    fragments are both conflict-free.  Filled by LDS-DMA (one 1-KiB wave-instruction per row,
+//    the swizzle applied to the per-lane SOURCE address, the LDS side linear).
+//  * Forward: 64-key tiles, K and V in one image each (K of tile j+1 lands during the P V of
+//    tile j, V of tile j+1 during the scores of tile j+1); online softmax with LAZY rescaling
+//    (the reference max is raised only when a row max exceeds it by > 8 in log2 units).
+//    LDS: K 64 KiB + V 64 KiB + exchange 32 KiB = 160 KiB.
+//  * Backward: 32-key tiles double-buffered (tile j+1's K and V land during tile j), scores and
+//    dP exchanged together.  LDS: 2 x (K 32 KiB + V 32 KiB) + exchange 32 KiB = 160 KiB.
+//  * Outputs (O, dQ) are staged through LDS and stored as whole 1-KiB rows.
+//  * Waits: raw s_barrier after an explicit lgkmcnt(0); LDS-DMA retired by vmcnt before the
+//    barrier that precedes the read (never __syncthreads, whose fence would drain the DMA).
+//  * XCD-aware block order: the q-tile blocks of one (n, h) share K / V through one XCD's L2.
 #include "common.h"
 
 namespace jmt {
 
-// A block is NW waves owning 16 NW rows; every block streams the whole K/V of its (n, h) through
-// LDS (attn_waves() picks NW).
-constexpr int AT_KT = 64;       // keys per tile
-constexpr int AT_FWD = 0, AT_DQ = 1;
+constexpr int AT_DH = 512;          // head dim of the fused kernels
+constexpr int AT_ROWB = 1024;       // bytes per image row (DH 16-bit values)
+constexpr int AT_QT = 64;           // rows per block
+constexpr int AF_KT = 64;           // forward keys per tile
+constexpr int AB_KT = 32;           // backward keys per tile
+constexpr int AT_XCH = 4096;        // exchange bytes per wave
+constexpr int AF_LDS = 2 * AF_KT * AT_ROWB + 8 * AT_XCH;   // 160 KiB
+constexpr int AB_LDS = 4 * AB_KT * AT_ROWB + 8 * AT_XCH;   // 160 KiB
 
-struct AttnParams {
-  const void* a;        // row operand: Q (fwd) / dO (dq)
-  const void* s1;       // score stream: K (fwd) / V (dq)
-  const void* s2;       // accumulate stream: V (fwd) / K (dq)
-  void* out;            // O (fwd) / dQ (dq)
-  const void* o_in;     // dq: forward output O (for rowsum(dO o O))
-  void* pbuf;           // fwd: unnormalised P out (nullable); dq: in, normalised P written back
-  void* dsbuf;          // dq: dS out
-  float* lse;           // fwd: out (nullable); dq: in
-  float* mt;            // per (row, key tile) reference max (fwd out, dq in) when pbuf is used
-  int64_t sa_l, sa_n, s1_l, s1_n, s2_l, s2_n, so_l, so_n, soi_l, soi_n, ldp;
-  int Lq, Lk, H;
-  float scale, scale_log2;
-};
+// byte offset of logical byte b of row `row` in a swizzled image
+__device__ __forceinline__ int img_off(int row, int b) {
+  return row * AT_ROWB + ((((b >> 4) ^ ((row & 7) << 1))) << 4) + (b & 15);
+}
+// output staging image (16-row swizzle: conflict-free ds_write_b64 of a 16-row fragment)
+__device__ __forceinline__ int out_off(int row, int b) {
+  return row * AT_ROWB + ((((b >> 4) ^ (row & 15))) << 4) + (b & 15);
+}
 
-template <int DH> struct AttnGeo {
-  static constexpr int RB = DH * 2;
-  static constexpr int PITCH = RB + 32;
-  static constexpr int IMG = AT_KT * PITCH;
-};
+// Per-lane base offsets of the fragment reads (the swizzle XOR touches chunk bits 1-3 only, so
+// a read's offset = one of a few lane bases + a compile-time immediate):
+//  row_base(m): ds_read_b128 fragment of row li (+16 kt), chunk 4 (4 a + m) + g of half h
+//               -> row_base(m) + 256 a + 16384 kt
+//  tr_base(c):  ds_read_b64_tr_b16 block rows 4 g + (li >> 2) (+16, +32 u), columns
+//               16 (8 b + c) + 4 (li & 3) of half h -> tr_base(c) + 256 b + 16384 hi + 32768 u
+__device__ __forceinline__ int row_base(int m, int li, int g, int h) {
+  return li * AT_ROWB + ((((4 * m + g) ^ ((li & 7) << 1))) << 4) + 512 * h;
+}
+__device__ __forceinline__ int tr_base(int c, int li, int g, int h) {
+  const int r = 4 * g + (li >> 2);
+  return r * AT_ROWB + ((((2 * c + ((li & 3) >> 1)) ^ ((r & 7) << 1))) << 4) + 8 * (li & 1) +
+         512 * h;
+}
 
-// stage one tile of AT_KT key rows (row r <- source row min(k0 + r, Lk - 1)): one 1-KiB
-// LDS-DMA wave-instruction per row (DH = 512)
-template <typename T, int DH, int NW>
-__device__ __forceinline__ void stage_kv(char* img, const T* base, int64_t ld, int k0, int Lk) {
-  typedef AttnGeo<DH> G;
-  static_assert(G::RB == 1024, "one LDS-DMA instruction per key row");
-  constexpr int NI = AT_KT / NW;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r0 = w * NI;
-  char* dst = img + r0 * G::PITCH;
-  if (k0 + AT_KT <= Lk) {          // whole tile in range: rows r0.. at a constant stride
-    const T* src = base + (int64_t)(k0 + r0) * ld + lane * 8;
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// stage R key rows k0.. (row r <- source row min(k0 + r, Lk - 1)) by LDS-DMA, R / 8 per wave.
+// Row addresses are wave-uniform (scalar arithmetic, saddr + 32-bit lane offset); the lane's
+// 16-B chunk is the swizzle of the image: LDS chunk `lane` of row r holds source chunk
+// lane ^ ((r & 7) << 1).
+template <typename T, int R, int NW = 8>
+__device__ __forceinline__ void stage_rows(char* img, const T* base, int64_t ld, int k0, int Lk) {
+  constexpr int NI = R / NW;
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
-    for (int i = 0; i < NI; ++i) glds16(src + i * ld, dst + i * G::PITCH);
-  } else {                         // last tile: rows past Lk repeat row Lk-1 (masked later)
-    const T* src = base + lane * 8;
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-      glds16(src + (int64_t)min(k0 + r0 + i, Lk - 1) * ld, dst + i * G::PITCH);
+  for (int i = 0; i < NI; ++i) {
+    const int r = wu * NI + i;
+    const int src = min(k0 + r, Lk - 1);
+    const char* row = (const char*)(base + (int64_t)src * ld);
+    const unsigned off = (unsigned)(lane ^ ((r & 7) << 1)) << 4;
+    glds16(row + off, img + r * AT_ROWB);
   }
 }
 
-template <typename T, int DH, int MODE, int NW>
-__global__ __launch_bounds__(64 * NW, 1) void attn_kernel(AttnParams p) {
-  constexpr int AT_QT = 16 * NW;                  // rows per block
-  typedef typename Frag16<T>::t F;
-  typedef typename Frag16<T>::h Hf;
-  typedef AttnGeo<DH> G;
-  constexpr int KS = DH / 32;                     // k-steps of the score product
-  constexpr int TD = DH / 16;                     // 16-column tiles of the accumulator
-  constexpr int NI = AT_KT / NW;                  // LDS-DMA instructions per wave per tile
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* img1 = smem;
-  char* img2 = smem + G::IMG;
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  // XCD-aware bijective remap: the q-tile blocks of one (n, h) share K/V through one XCD's L2
-  const int nqt = (p.Lq + AT_QT - 1) / AT_QT;
+// XCD-aware bijective remap of the block index (blocks % 8 share an XCD)
+__device__ __forceinline__ int xcd_block() {
   const int nwg = gridDim.x;
   int wg = blockIdx.x;
   if (nwg >= 16) {
     const int qd = nwg / 8, rm = nwg % 8, x = blockIdx.x % 8;
     wg = (x < rm ? x * (qd + 1) : rm * (qd + 1) + (x - rm) * qd) + blockIdx.x / 8;
   }
-  const int nh = wg / nqt;
-  const int n = nh / p.H, h = nh % p.H;
-  const int q0 = (wg % nqt) * AT_QT;
-  const T* ab = (const T*)p.a + (int64_t)n * p.sa_n + h * DH;
-  const T* s1b = (const T*)p.s1 + (int64_t)n * p.s1_n + h * DH;
-  const T* s2b = (const T*)p.s2 + (int64_t)n * p.s2_n + h * DH;
-  const int nkt = (p.Lk + AT_KT - 1) / AT_KT;
+  return wg;
+}
 
-  // this lane's row and its row-operand fragments (rows past Lq read row Lq-1, never stored)
-  const int qr = q0 + 16 * w + li;
-  const int qc = min(qr, p.Lq - 1);
-  F qf[KS];
-  {
-    const T* arow = ab + (int64_t)qc * p.sa_l;
+// store this wave's 16 x 256 accumulator half (lane: row li, dims 256 h + 16 t + 4 g + r,
+// multiplied by `mul`) through the LDS staging image, then whole rows to global memory.
+// Every wave must have finished reading the LDS region before the call.
+template <typename T>
+__device__ __forceinline__ void store_rows(char* stage, const f32x4* acc, float mul, T* out,
+                                           int64_t so_l, int q0, int Lq) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15, rg = w & 3, h = w >> 2;
+  const int row = 16 * rg + li;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) qf[ks] = *(const F*)(arow + 32 * ks + 8 * g);
+  for (int t = 0; t < 16; ++t) {
+    T v4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v4[r] = from_f<T>(acc[t][r] * mul);
+    *(uint2*)(stage + out_off(row, (256 * h + 16 * t + 4 * g) * 2)) = *(const uint2*)v4;
   }
-  const int64_t prow = ((int64_t)nh * p.Lq + qc);          // row index into P / dS / lse / mt
-  float delta = 0.f, lse2 = 0.f;
-  F of[MODE == AT_DQ ? KS : 1];
-  if constexpr (MODE == AT_DQ) {
-    const T* orow = (const T*)p.o_in + (int64_t)qc * p.soi_l + (int64_t)n * p.soi_n + h * DH;
+  lds_barrier();
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) of[ks] = *(const F*)(orow + 32 * ks + 8 * g);
-    lse2 = p.lse[prow] * 1.4426950408889634f;
-  }
-  // tile-0 DMA is issued behind the row loads (vmcnt retires in issue order)
-  stage_kv<T, DH, NW>(img1, s1b, p.s1_l, 0, p.Lk);
-  stage_kv<T, DH, NW>(img2, s2b, p.s2_l, 0, p.Lk);
-  if constexpr (MODE == AT_DQ) {
-    // Delta = rowsum(dO o O) = rowsum(P o dP)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) delta += (float)of[ks][e] * (float)qf[ks][e];
-    delta += __shfl_xor(delta, 16, 64);
-    delta += __shfl_xor(delta, 32, 64);
-  }
-
-  f32x4 o[TD];
-#pragma unroll
-  for (int t = 0; t < TD; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
-
-  // per-lane fragment bases: stream-1 rows 16kt + li, chunk 4ks + g; stream-2 transpose-read
-  // rows 32u + 4g + (li>>2) (+16 for the upper k-slots), columns 16t + 4(li&3)
-  const char* s1l = img1 + li * G::PITCH + g * 16;
-  const char* s2l = img2 + (4 * g + (li >> 2)) * G::PITCH + 8 * (li & 3);
-  T* prow_p = (T*)p.pbuf + prow * p.ldp;
-  T* prow_ds = (T*)p.dsbuf + prow * p.ldp;
-  uint2 pin[4];                                   // dq: this tile's unnormalised P (4 x 4 keys)
-  float mref = 0.f;                               // dq: this tile's reference max
-  auto load_p = [&](int j) {
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      const int key = AT_KT * j + 16 * kt + 4 * g;
-      pin[kt] = key < p.ldp ? *(const uint2*)(prow_p + key) : make_uint2(0u, 0u);
+  for (int i = 0; i < 8; ++i) {
+    const int r = 8 * w + i;
+    if (q0 + r < Lq) {
+      const uint4 v = *(const uint4*)(stage + out_off(r, lane * 16));
+      *(uint4*)(out + (int64_t)(q0 + r) * so_l + lane * 8) = v;
     }
-    mref = p.mt[prow * nkt + j];
-  };
-  if constexpr (MODE == AT_DQ) load_p(0);
+  }
+}
 
-  wait_vmcnt<NI>();                               // stream-1 tile 0 landed (tile-0 stream 2 in flight)
-  __syncthreads();
+struct AttnFwdArgs {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  float* lse;
+  int64_t sq_l, sq_n, sk_l, sk_n, sv_l, sv_n, so_l, so_n;
+  int Lq, Lk, H;
+  float scale_log2;
+  uint64_t* stamps;
+};
+
+// Phase stamps (diagnostic build only, STAMP = true): s_memtime at each phase boundary of every
+// tile of one block in the middle of the grid, stored by every lane of waves 0 and 4 at a
+// lane-indexed address (vector stores).
+template <bool STAMP>
+__device__ __forceinline__ void stamp(uint64_t* buf, int idx) {
+  if constexpr (STAMP) {
+    if (buf && blockIdx.x == gridDim.x / 2 && ((threadIdx.x >> 6) & 3) == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      buf[((threadIdx.x >> 8) * 256 + idx) * 64 + (threadIdx.x & 63)] = t;
+    }
+  }
+}
+
+template <typename T, bool STAMP = false>
+__global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
+  typedef typename Frag16<T>::t F;
+  typedef typename Frag16<T>::h Hf;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* kimg = smem;
+  char* vimg = smem + AF_KT * AT_ROWB;
+  char* xch = smem + 2 * AF_KT * AT_ROWB;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15, rg = w & 3, h = w >> 2;
+  const int nqt = (p.Lq + AT_QT - 1) / AT_QT;
+  const int wg = xcd_block();
+  const int nh = wg / nqt;
+  const int n = nh / p.H, hd = nh % p.H;
+  const int q0 = (wg % nqt) * AT_QT;
+  const T* kb = (const T*)p.k + (int64_t)n * p.sk_n + hd * AT_DH;
+  const T* vb = (const T*)p.v + (int64_t)n * p.sv_n + hd * AT_DH;
+  const int nkt = (p.Lk + AF_KT - 1) / AF_KT;
+
+  const int qr = q0 + 16 * rg + li;
+  F qf[8];
+  {
+    const T* qrow = (const T*)p.q + (int64_t)n * p.sq_n + hd * AT_DH +
+                    (int64_t)min(qr, p.Lq - 1) * p.sq_l + 256 * h + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const F*)(qrow + 32 * ks);
+  }
+  stage_rows<T, AF_KT>(kimg, kb, p.sk_l, 0, p.Lk);
+  stage_rows<T, AF_KT>(vimg, vb, p.sv_l, 0, p.Lk);
+
+  f32x4 o[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4* xmine = (f32x4*)(xch + w * AT_XCH) + lane;
+  const f32x4* xpart = (const f32x4*)(xch + (w ^ 4) * AT_XCH) + lane;
+  int kb4[4], tb8[8];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) kb4[m] = row_base(m, li, g, h);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) tb8[c] = tr_base(c, li, g, h);
+
+  wait_vmcnt<AF_KT / 8>();                        // Q and K tile 0 landed (V 0 in flight)
+  lds_barrier();
+  stamp<STAMP>(p.stamps, 255);
   for (int j = 0; j < nkt; ++j) {
-    // ---- score tile: s[kt][r] = <row qr, key 64j + 16kt + 4g + r>
+    stamp<STAMP>(p.stamps, 8 * j);
+    // ---- partial scores over this wave's 256 dims: s[kt][r] = <row qr, key 64j+16kt+4g+r>
     f32x4 s[4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    {   // score fragments double-buffered: k-step ks+1's reads issue before k-step ks's MFMAs
-      F kf[2][4];
+    {   // k-step batches of 4 fragments (key subtiles 0..3), double-buffered: the reads of
+        // batch ks+1 are in flight while the 4 MFMAs of batch ks run (pinned by sched_barrier)
+      F fa[4], fb[4];
+      auto kbatch = [&](F* dst, int ks) {
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) kf[0][kt] = *(const F*)(s1l + kt * 16 * G::PITCH);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        if (ks + 1 < KS) {
-#pragma unroll
-          for (int kt = 0; kt < 4; ++kt)
-            kf[(ks + 1) & 1][kt] = *(const F*)(s1l + kt * 16 * G::PITCH + (ks + 1) * 64);
-        }
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) s[kt] = mfma16(kf[ks & 1][kt], qf[ks], s[kt]);
-      }
-    }
-    const int kbase = AT_KT * j + 4 * g;
-    F pf[2];
-    if constexpr (MODE == AT_FWD) {
-      // ---- online softmax (log2 domain); keys >= Lk masked
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float x = (kbase + 16 * kt + r < p.Lk) ? s[kt][r] * p.scale_log2 : -INFINITY;
-          s[kt][r] = x;
-          mx = fmaxf(mx, x);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      if (__any(mx > m_run + 8.f)) {              // lazy rescale (see header)
-        const float m_new = fmaxf(m_run, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-        m_run = m_new;
-        l_run *= alpha;
-#pragma unroll
-        for (int t = 0; t < TD; ++t) o[t] *= alpha;
-      }
-      float ls = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(s[kt][r] - m_run);
-          ls += pv;
-          pf[kt >> 1][(kt & 1) * 4 + r] = from_f<T>(pv);
-        }
-      l_run += ls;
-      if (p.pbuf && qr < p.Lq) {
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
-          const int key = kbase + 16 * kt;
-          if (key < p.ldp) {
-            T v4[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v4[r] = pf[kt >> 1][(kt & 1) * 4 + r];
-            *(uint2*)(prow_p + key) = *(const uint2*)v4;
-          }
-        }
-        if (g == 0) p.mt[prow * nkt + j] = m_run;
-      }
-    } else {
-      // ---- dS = scale * P o (dP - Delta), P = Ptilde * 2^(mref - lse); P written back exact
-      const float f = __builtin_amdgcn_exp2f(mref - lse2);
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const T* pt = (const T*)&pin[kt];
-        T pn[4], dsv[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = (float)pt[r] * f;
-          pn[r] = from_f<T>(pv);
-          const float ds = p.scale * pv * (s[kt][r] - delta);
-          dsv[r] = from_f<T>(ds);
-          pf[kt >> 1][(kt & 1) * 4 + r] = dsv[r];
-        }
-        const int key = kbase + 16 * kt;
-        if (qr < p.Lq && key < p.ldp) {
-          *(uint2*)(prow_p + key) = *(const uint2*)pn;
-          *(uint2*)(prow_ds + key) = *(const uint2*)dsv;
-        }
-      }
-    }
-
-    wait_vmcnt<0>();                              // stream-2 tile j landed
-    __syncthreads();                              // ... for all waves; stream-1 image free
-    if (j + 1 < nkt) {
-      stage_kv<T, DH, NW>(img1, s1b, p.s1_l, AT_KT * (j + 1), p.Lk);
-      if constexpr (MODE == AT_DQ) load_p(j + 1);
-    }
-
-    // ---- accumulate: acc[t] += sum_k pf(k) * stream2[k][16t + 4g + r]
-    // fragment reads run PD MFMAs ahead (a ring of PD fragments): the transposed LDS reads of
-    // fragment q+PD are in flight while MFMA q executes, instead of one read->wait->MFMA chain
-    {
-      constexpr int NQ = 2 * TD, PD = 4;
-      auto vread = [&](int q) -> F {
-        const int u = q / TD, t = q % TD;
-        const Hf lo = tr_read<Hf>(s2l + 32 * u * G::PITCH + 32 * t);
-        const Hf hi = tr_read<Hf>(s2l + (32 * u + 16) * G::PITCH + 32 * t);
-        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        for (int kt = 0; kt < 4; ++kt)
+          dst[kt] = *(const F*)(kimg + kb4[ks & 3] + 256 * (ks >> 2) + 16384 * kt);
       };
-      F ring[PD];
+      kbatch(fa, 0);
 #pragma unroll
-      for (int q = 0; q < PD; ++q) ring[q] = vread(q);
+      for (int ks = 0; ks < 8; ks += 2) {
+        kbatch(fb, ks + 1);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const F vf = ring[q % PD];
-        if (q + PD < NQ) ring[q % PD] = vread(q + PD);
-        o[q % TD] = mfma16(vf, pf[q / TD], o[q % TD]);
+        for (int kt = 0; kt < 4; ++kt) s[kt] = mfma16(fa[kt], qf[ks], s[kt]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + 2 < 8) kbatch(fa, ks + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) s[kt] = mfma16(fb[kt], qf[ks + 1], s[kt]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
+    stamp<STAMP>(p.stamps, 8 * j + 1);
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) xmine[64 * kt] = s[kt];
+    wait_vmcnt<0>();                              // V tile j landed
+    stamp<STAMP>(p.stamps, 8 * j + 2);
+    lds_barrier();                                // partials visible; K image free
+    stamp<STAMP>(p.stamps, 8 * j + 3);
+    if (j + 1 < nkt) stage_rows<T, AF_KT>(kimg, kb, p.sk_l, AF_KT * (j + 1), p.Lk);
+    const int kbase = AF_KT * j + 4 * g;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const f32x4 ps = xpart[64 * kt];
+      const f32x4 full = h == 0 ? s[kt] + ps : ps + s[kt];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = (kbase + 16 * kt + r < p.Lk) ? full[r] * p.scale_log2 : -INFINITY;
+        s[kt][r] = x;
+        mx = fmaxf(mx, x);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (__any(mx > m_run + 8.f)) {                // lazy rescale (header)
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      m_run = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) o[t] *= alpha;
+    }
+    F pf[2];
+    float ls = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(s[kt][r] - m_run);
+        ls += pv;
+        pf[kt >> 1][(kt & 1) * 4 + r] = from_f<T>(pv);
+      }
+    l_run += ls;
+    stamp<STAMP>(p.stamps, 8 * j + 4);
+    // ---- o[t] += sum_k P(k) V[k][256h + 16t + 4g + r]: transposed fragment reads of the V
+    // image in double-buffered batches of 4 fragments (q = 4b + i: t = q % 16, u = q / 16)
+    {
+      F fa[4], fb[4];
+      auto vbatch = [&](F* dst, int b) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = 4 * b + i, u = q >> 4, t = q & 15;
+          const char* a = vimg + tb8[t & 7] + 256 * (t >> 3) + 32768 * u;
+          const Hf lo = tr_read<Hf>(a);
+          const Hf hi = tr_read<Hf>(a + 16384);
+          dst[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      };
+      vbatch(fa, 0);
+#pragma unroll
+      for (int b = 0; b < 8; b += 2) {
+        vbatch(fb, b + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = 4 * b + i;
+          o[q & 15] = mfma16(fa[i], pf[q >> 4], o[q & 15]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (b + 2 < 8) vbatch(fa, b + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = 4 * (b + 1) + i;
+          o[q & 15] = mfma16(fb[i], pf[q >> 4], o[q & 15]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    stamp<STAMP>(p.stamps, 8 * j + 5);
     if (j + 1 < nkt) {
-      wait_vmcnt<0>();                            // stream-1 tile j+1 landed
-      __syncthreads();                            // ... for all waves; stream-2 image free
-      stage_kv<T, DH, NW>(img2, s2b, p.s2_l, AT_KT * (j + 1), p.Lk);
+      wait_vmcnt<0>();                            // K tile j+1 landed
+      stamp<STAMP>(p.stamps, 8 * j + 6);
+      lds_barrier();                              // V image and exchange slots free
+      stage_rows<T, AF_KT>(vimg, vb, p.sv_l, AF_KT * (j + 1), p.Lk);
     }
   }
+  stamp<STAMP>(p.stamps, 254);
+  float lt = l_run;
+  lt += __shfl_xor(lt, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+  if (qr < p.Lq && g == 0 && h == 0 && p.lse)
+    p.lse[(int64_t)nh * p.Lq + qr] = (m_run + __builtin_amdgcn_logf(lt)) * 0.69314718055994531f;
+  lds_barrier();                                  // every wave is done with the V image
+  store_rows<T>(kimg, o, 1.f / lt,
+                (T*)p.o + (int64_t)n * p.so_n + hd * AT_DH, p.so_l, q0, p.Lq);
+}
 
-  // ---- store: lane owns row qr, columns 16t + 4g .. +3
-  float inv = 1.f;
-  if constexpr (MODE == AT_FWD) {
-    float lt = l_run;
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
-    inv = 1.f / lt;
-    if (qr < p.Lq && g == 0 && p.lse)
-      p.lse[prow] = (m_run + __builtin_amdgcn_logf(lt)) * 0.69314718055994531f;
-  }
-  if (qr < p.Lq) {
-    T* orow = (T*)p.out + (int64_t)qr * p.so_l + (int64_t)n * p.so_n + h * DH;
+
+// (A 4-wave, one-wave-per-SIMD forward with v_mfma_f32_32x32x16, 32 rows x all 512 dims per wave
+// and 128 rows per block — half the K/V bytes into LDS and half the LDS fragment bytes per FLOP —
+// needs ~480 registers per wave (O 256 + Q 128 + working set) and spilled 256 VGPRs under hipcc:
+// not kept.  Phase stamps of this 16x16 kernel: profiles/r02_attn_phase_stamps.txt.)
+
+struct AttnBwdArgs {
+  const void* go;
+  const void* o;
+  const void* q;
+  const void* k;
+  const void* v;
+  const float* lse;
+  void* pbuf;
+  void* dsbuf;
+  void* dq;
+  int64_t sgo_l, sgo_n, so_l, so_n, sq_l, sq_n, sk_l, sk_n, sv_l, sv_n, sdq_l, sdq_n, ldp;
+  int Lq, Lk, H;
+  float scale, scale_log2;
+};
+
+template <typename T>
+__global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
+  typedef typename Frag16<T>::t F;
+  typedef typename Frag16<T>::h Hf;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int IMG = AB_KT * AT_ROWB;            // one K or V image
+  char* xch = smem + 4 * IMG;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15, rg = w & 3, h = w >> 2;
+  const int nqt = (p.Lq + AT_QT - 1) / AT_QT;
+  const int wg = xcd_block();
+  const int nh = wg / nqt;
+  const int n = nh / p.H, hd = nh % p.H;
+  const int q0 = (wg % nqt) * AT_QT;
+  const T* kb = (const T*)p.k + (int64_t)n * p.sk_n + hd * AT_DH;
+  const T* vb = (const T*)p.v + (int64_t)n * p.sv_n + hd * AT_DH;
+  const int nkt = (p.Lk + AB_KT - 1) / AB_KT;
+
+  const int qr = q0 + 16 * rg + li;
+  const int qc = min(qr, p.Lq - 1);
+  const int64_t prow = (int64_t)nh * p.Lq + qc;
+  F qf[8], df[8];
+  float delta;
+  {
+    const int64_t coff = (int64_t)hd * AT_DH + 256 * h + 8 * g;
+    const T* qrow = (const T*)p.q + (int64_t)n * p.sq_n + (int64_t)qc * p.sq_l + coff;
+    const T* drow = (const T*)p.go + (int64_t)n * p.sgo_n + (int64_t)qc * p.sgo_l + coff;
+    const T* orow = (const T*)p.o + (int64_t)n * p.so_n + (int64_t)qc * p.so_l + coff;
+    float dp = 0.f;
 #pragma unroll
-    for (int t = 0; t < TD; ++t) {
-      T v4[4];
+    for (int ks = 0; ks < 8; ++ks) {
+      qf[ks] = *(const F*)(qrow + 32 * ks);
+      df[ks] = *(const F*)(drow + 32 * ks);
+      const F of = *(const F*)(orow + 32 * ks);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v4[r] = from_f<T>(o[t][r] * inv);
-      *(uint2*)(orow + 16 * t + 4 * g) = *(const uint2*)v4;
+      for (int e = 0; e < 8; ++e) dp += (float)of[e] * (float)df[ks][e];
     }
+    dp += __shfl_xor(dp, 16, 64);
+    dp += __shfl_xor(dp, 32, 64);
+    delta = dp;                                   // this half's part of rowsum(dO o O)
   }
+  const float lse2 = p.lse[prow] * 1.4426950408889634f;
+  stage_rows<T, AB_KT>(smem, kb, p.sk_l, 0, p.Lk);
+  stage_rows<T, AB_KT>(smem + IMG, vb, p.sv_l, 0, p.Lk);
+  ((float*)xch)[w * 64 + lane] = delta;
+
+  f32x4 acc[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4* xmine = (f32x4*)(xch + w * AT_XCH) + lane;
+  const f32x4* xpart = (const f32x4*)(xch + (w ^ 4) * AT_XCH) + lane;
+  T* prow_p = (T*)p.pbuf + prow * p.ldp;
+  T* prow_ds = (T*)p.dsbuf + prow * p.ldp;
+  int kb4[4], tb8[8];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) kb4[m] = row_base(m, li, g, h);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) tb8[c] = tr_base(c, li, g, h);
+
+  wait_vmcnt<0>();                                // tile 0 landed
+  lds_barrier();                                  // ... and every Delta part written
+  {
+    const float part = ((const float*)xch)[(w ^ 4) * 64 + lane];
+    delta = h == 0 ? delta + part : part + delta;
+  }
+  lds_barrier();                                  // Delta parts read: exchange slots free
+
+  for (int j = 0; j < nkt; ++j) {
+    const char* kimg = smem + (j & 1) * 2 * IMG;
+    const char* vimg = kimg + IMG;
+    if (j + 1 < nkt) {                            // tile j+1 into the other buffer pair
+      char* nk = smem + ((j + 1) & 1) * 2 * IMG;
+      stage_rows<T, AB_KT>(nk, kb, p.sk_l, AB_KT * (j + 1), p.Lk);
+      stage_rows<T, AB_KT>(nk + IMG, vb, p.sv_l, AB_KT * (j + 1), p.Lk);
+    }
+    // ---- partial scores (K) and partial dP (V) over this wave's 256 dims
+    f32x4 s[2], d[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      d[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    {   // k-step batches (K and V fragments of key subtiles 0, 1), double-buffered
+      F fa[4], fb[4];
+      auto batch = [&](F* dst, int ks) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const int o = kb4[ks & 3] + 256 * (ks >> 2) + 16384 * kt;
+          dst[kt] = *(const F*)(kimg + o);
+          dst[2 + kt] = *(const F*)(vimg + o);
+        }
+      };
+      batch(fa, 0);
+#pragma unroll
+      for (int ks = 0; ks < 8; ks += 2) {
+        batch(fb, ks + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          s[kt] = mfma16(fa[kt], qf[ks], s[kt]);
+          d[kt] = mfma16(fa[2 + kt], df[ks], d[kt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + 2 < 8) batch(fa, ks + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          s[kt] = mfma16(fb[kt], qf[ks + 1], s[kt]);
+          d[kt] = mfma16(fb[2 + kt], df[ks + 1], d[kt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    xmine[0] = s[0];
+    xmine[64] = s[1];
+    xmine[128] = d[0];
+    xmine[192] = d[1];
+    lds_barrier();                                // partials visible (tile j+1 DMA in flight)
+    const int kbase = AB_KT * j + 4 * g;
+    F dsf;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const f32x4 ps = xpart[64 * kt], pd = xpart[128 + 64 * kt];
+      const f32x4 sf = h == 0 ? s[kt] + ps : ps + s[kt];
+      const f32x4 dfull = h == 0 ? d[kt] + pd : pd + d[kt];
+      T pv4[4], ds4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool in = kbase + 16 * kt + r < p.Lk;
+        const float pv = in ? __builtin_amdgcn_exp2f(sf[r] * p.scale_log2 - lse2) : 0.f;
+        const float ds = p.scale * pv * (dfull[r] - delta);
+        pv4[r] = from_f<T>(pv);
+        ds4[r] = from_f<T>(ds);
+        dsf[kt * 4 + r] = ds4[r];
+      }
+      const int key = kbase + 16 * kt;
+      if (qr < p.Lq && key < p.ldp) {
+        if (h == 0) *(uint2*)(prow_p + key) = *(const uint2*)pv4;
+        else *(uint2*)(prow_ds + key) = *(const uint2*)ds4;
+      }
+    }
+    // ---- acc[t] += sum_k dS(k) K[k][256h + 16t + 4g + r] (transposed K fragments in
+    // double-buffered batches of 4)
+    {
+      F fa[4], fb[4];
+      auto kbatch = [&](F* dst, int b) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = 4 * b + i;
+          const char* a = kimg + tb8[t & 7] + 256 * (t >> 3);
+          const Hf lo = tr_read<Hf>(a);
+          const Hf hi = tr_read<Hf>(a + 16384);
+          dst[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      };
+      kbatch(fa, 0);
+#pragma unroll
+      for (int b = 0; b < 4; b += 2) {
+        kbatch(fb, b + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[4 * b + i] = mfma16(fa[i], dsf, acc[4 * b + i]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (b + 2 < 4) kbatch(fa, b + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[4 * b + 4 + i] = mfma16(fb[i], dsf, acc[4 * b + 4 + i]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    wait_vmcnt<0>();                              // tile j+1 landed (and P / dS stores issued)
+    lds_barrier();                                // this buffer pair and the slots are free
+  }
+  store_rows<T>(smem, acc, 1.f, (T*)p.dq + (int64_t)n * p.sdq_n + hd * AT_DH, p.sdq_l, q0,
+                p.Lq);
 }
 
-// waves per block: 4.  8-wave blocks (half the K/V staging per FLOP) measured 3-33% SLOWER at
-// T = 300 (fwd 290 vs 280 us, dQ 400 vs 352 us for the 6 cross-attention pairs at B = 64), so the
-// kernel is not K/V-load-bound there; NW stays a template parameter for other shapes.
-static int attn_waves(int) { return 4; }
-
-template <typename T, int DH, int MODE, int NW>
-static void launch_nw(const AttnParams& p, int N, hipStream_t st) {
-  constexpr int LDS = 2 * AttnGeo<DH>::IMG;
-  auto fn = attn_kernel<T, DH, MODE, NW>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr = true;
-  }
-  dim3 grid((unsigned)(((p.Lq + 16 * NW - 1) / (16 * NW)) * N * p.H));
-  hipLaunchKernelGGL(fn, grid, dim3(64 * NW), (size_t)LDS, st, p);
-}
-
-template <typename T, int DH, int MODE>
-static void launch(const AttnParams& p, int N, hipStream_t st) {
-  (void)attn_waves(p.Lq);
-  launch_nw<T, DH, MODE, 4>(p, N, st);
+template <typename K>
+static void set_lds(K fn, int bytes) {
+  (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
 static int check_common(const char* name, int N, int H, int Lq, int Lk, const void* const* ptrs,
                         int nptr, const int64_t* strides, int nstr) {
   JMT_CHECK_ARG(N > 0 && H > 0 && Lq > 0 && Lk > 0 &&
-                    (int64_t)N * H * ((Lq + 63) / 64) < (1LL << 31),
+                    (int64_t)N * H * ((Lq + AT_QT - 1) / AT_QT) < (1LL << 31),
                 "%s: bad sizes", name);
   for (int i = 0; i < nptr; ++i)
     JMT_CHECK_ARG(ptrs[i] != nullptr && ((uintptr_t)ptrs[i] & 15) == 0,
@@ -353,19 +555,23 @@ static int check_common(const char* name, int N, int H, int Lq, int Lk, const vo
 
 using namespace jmt;
 
-extern "C" int jmt_attn_supported(int dt, int dh) {
-  return (dt == JMT_BF16 || dt == JMT_F16) && dh == 512;
+static void* g_stamps = nullptr;
+
+// diagnostic: route jmt_attn_fwd (bf16) through the phase-stamped kernel, stamps into `buf`
+// (2 x 256 x 64 uint64); NULL turns it off.  Not part of include/jmt.h (dev tool).
+extern "C" int jmt_attn_set_stamps(void* buf) {
+  g_stamps = buf;
+  return JMT_OK;
 }
 
-extern "C" int jmt_attn_mt_floats(int N, int H, int Lq, int Lk) {
-  return N * H * Lq * ((Lk + AT_KT - 1) / AT_KT);
+extern "C" int jmt_attn_supported(int dt, int dh) {
+  return (dt == JMT_BF16 || dt == JMT_F16) && dh == AT_DH;
 }
 
 extern "C" int jmt_attn_fwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* q,
                             int64_t sq_l, int64_t sq_n, const void* k, int64_t sk_l, int64_t sk_n,
                             const void* v, int64_t sv_l, int64_t sv_n, void* o, int64_t so_l,
-                            int64_t so_n, float scale, float* lse, void* p_out, int64_t ldp,
-                            float* mt, void* stream) {
+                            int64_t so_n, float scale, float* lse, void* stream) {
   if (N == 0 || Lq == 0) return JMT_OK;
   if (!jmt_attn_supported(dt, dh))
     return set_error(JMT_ERR_UNSUPPORTED, "jmt_attn_fwd: dtype %d / head dim %d not supported",
@@ -374,48 +580,69 @@ extern "C" int jmt_attn_fwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
   const int64_t strides[] = {sq_l, sq_n, sk_l, sk_n, sv_l, sv_n, so_l, so_n};
   int rc = check_common("jmt_attn_fwd", N, H, Lq, Lk, ptrs, 4, strides, 8);
   if (rc != JMT_OK) return rc;
-  JMT_CHECK_ARG(!p_out || (mt && ldp >= Lk && ldp % 8 == 0 && ((uintptr_t)p_out & 15) == 0),
-                "jmt_attn_fwd: P output needs mt, ldp >= Lk, ldp %% 8 == 0, 16-B alignment");
-  AttnParams p = {};
-  p.a = q; p.s1 = k; p.s2 = v; p.out = o; p.lse = lse; p.pbuf = p_out; p.mt = mt;
-  p.sa_l = sq_l; p.sa_n = sq_n; p.s1_l = sk_l; p.s1_n = sk_n; p.s2_l = sv_l; p.s2_n = sv_n;
-  p.so_l = so_l; p.so_n = so_n; p.ldp = ldp;
-  p.Lq = Lq; p.Lk = Lk; p.H = H;
-  p.scale = scale;
-  p.scale_log2 = scale * 1.4426950408889634f;
+  AttnFwdArgs a = {};
+  a.q = q; a.k = k; a.v = v; a.o = o; a.lse = lse;
+  a.sq_l = sq_l; a.sq_n = sq_n; a.sk_l = sk_l; a.sk_n = sk_n; a.sv_l = sv_l; a.sv_n = sv_n;
+  a.so_l = so_l; a.so_n = so_n;
+  a.Lq = Lq; a.Lk = Lk; a.H = H;
+  a.scale_log2 = scale * 1.4426950408889634f;
   hipStream_t st = as_stream(stream);
-  if (dt == JMT_BF16) launch<__bf16, 512, AT_FWD>(p, N, st);
-  else launch<_Float16, 512, AT_FWD>(p, N, st);
+  const dim3 grid((unsigned)(((Lq + AT_QT - 1) / AT_QT) * N * H));
+  if (g_stamps && dt == JMT_BF16) {   // diagnostic: phase stamps (jmt_attn_set_stamps)
+    a.stamps = (uint64_t*)g_stamps;
+    static bool once = (set_lds(attn_fwd_kernel<__bf16, true>, AF_LDS), true);
+    (void)once;
+    hipLaunchKernelGGL((attn_fwd_kernel<__bf16, true>), grid, dim3(512), (size_t)AF_LDS, st, a);
+  } else if (dt == JMT_BF16) {
+    static bool once = (set_lds(attn_fwd_kernel<__bf16>, AF_LDS), true);
+    (void)once;
+    hipLaunchKernelGGL(attn_fwd_kernel<__bf16>, grid, dim3(512), (size_t)AF_LDS, st, a);
+  } else {
+    static bool once = (set_lds(attn_fwd_kernel<_Float16>, AF_LDS), true);
+    (void)once;
+    hipLaunchKernelGGL(attn_fwd_kernel<_Float16>, grid, dim3(512), (size_t)AF_LDS, st, a);
+  }
   JMT_LAUNCH_CHECK("jmt_attn_fwd");
   return JMT_OK;
 }
 
-extern "C" int jmt_attn_bwd_dq(int dt, int N, int H, int Lq, int Lk, int dh, const void* go,
-                               int64_t sgo_l, int64_t sgo_n, const void* o, int64_t so_l,
-                               int64_t so_n, const void* k, int64_t sk_l, int64_t sk_n,
-                               const void* v, int64_t sv_l, int64_t sv_n, const float* lse,
-                               void* p_buf, const float* mt, int64_t ldp, void* ds, void* dq,
-                               int64_t sdq_l, int64_t sdq_n, float scale, void* stream) {
+extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* go,
+                            int64_t sgo_l, int64_t sgo_n, const void* o, int64_t so_l,
+                            int64_t so_n, const void* q, int64_t sq_l, int64_t sq_n,
+                            const void* k, int64_t sk_l, int64_t sk_n, const void* v,
+                            int64_t sv_l, int64_t sv_n, const float* lse, void* p_out,
+                            void* ds_out, int64_t ldp, void* dq, int64_t sdq_l, int64_t sdq_n,
+                            float scale, void* stream) {
   if (N == 0 || Lq == 0) return JMT_OK;
   if (!jmt_attn_supported(dt, dh))
-    return set_error(JMT_ERR_UNSUPPORTED, "jmt_attn_bwd_dq: dtype %d / head dim %d not supported",
+    return set_error(JMT_ERR_UNSUPPORTED, "jmt_attn_bwd: dtype %d / head dim %d not supported",
                      dt, dh);
-  const void* ptrs[] = {go, o, k, v, p_buf, ds, dq};
-  const int64_t strides[] = {sgo_l, sgo_n, so_l, so_n, sk_l, sk_n, sv_l, sv_n, sdq_l, sdq_n, ldp};
-  int rc = check_common("jmt_attn_bwd_dq", N, H, Lq, Lk, ptrs, 7, strides, 11);
+  const void* ptrs[] = {go, o, q, k, v, p_out, ds_out, dq};
+  const int64_t strides[] = {sgo_l, sgo_n, so_l, so_n, sq_l, sq_n, sk_l, sk_n, sv_l, sv_n,
+                             sdq_l, sdq_n, ldp};
+  int rc = check_common("jmt_attn_bwd", N, H, Lq, Lk, ptrs, 8, strides, 13);
   if (rc != JMT_OK) return rc;
-  JMT_CHECK_ARG(lse && mt && ldp >= Lk, "jmt_attn_bwd_dq: lse / mt missing or ldp < Lk");
-  AttnParams p = {};
-  p.a = go; p.s1 = v; p.s2 = k; p.out = dq; p.o_in = o; p.pbuf = p_buf; p.dsbuf = ds;
-  p.lse = const_cast<float*>(lse); p.mt = const_cast<float*>(mt);
-  p.sa_l = sgo_l; p.sa_n = sgo_n; p.s1_l = sv_l; p.s1_n = sv_n; p.s2_l = sk_l; p.s2_n = sk_n;
-  p.so_l = sdq_l; p.so_n = sdq_n; p.soi_l = so_l; p.soi_n = so_n; p.ldp = ldp;
-  p.Lq = Lq; p.Lk = Lk; p.H = H;
-  p.scale = scale;
-  p.scale_log2 = scale * 1.4426950408889634f;
+  JMT_CHECK_ARG(lse && ldp >= Lk, "jmt_attn_bwd: lse missing or ldp < Lk");
+  AttnBwdArgs a = {};
+  a.go = go; a.o = o; a.q = q; a.k = k; a.v = v; a.lse = lse;
+  a.pbuf = p_out; a.dsbuf = ds_out; a.dq = dq;
+  a.sgo_l = sgo_l; a.sgo_n = sgo_n; a.so_l = so_l; a.so_n = so_n; a.sq_l = sq_l; a.sq_n = sq_n;
+  a.sk_l = sk_l; a.sk_n = sk_n; a.sv_l = sv_l; a.sv_n = sv_n; a.sdq_l = sdq_l; a.sdq_n = sdq_n;
+  a.ldp = ldp;
+  a.Lq = Lq; a.Lk = Lk; a.H = H;
+  a.scale = scale;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  const dim3 grid((unsigned)(((Lq + AT_QT - 1) / AT_QT) * N * H));
   hipStream_t st = as_stream(stream);
-  if (dt == JMT_BF16) launch<__bf16, 512, AT_DQ>(p, N, st);
-  else launch<_Float16, 512, AT_DQ>(p, N, st);
-  JMT_LAUNCH_CHECK("jmt_attn_bwd_dq");
+  if (dt == JMT_BF16) {
+    static bool once = (set_lds(attn_bwd_kernel<__bf16>, AB_LDS), true);
+    (void)once;
+    hipLaunchKernelGGL(attn_bwd_kernel<__bf16>, grid, dim3(512), (size_t)AB_LDS, st, a);
+  } else {
+    static bool once = (set_lds(attn_bwd_kernel<_Float16>, AB_LDS), true);
+    (void)once;
+    hipLaunchKernelGGL(attn_bwd_kernel<_Float16>, grid, dim3(512), (size_t)AB_LDS, st, a);
+  }
+  JMT_LAUNCH_CHECK("jmt_attn_bwd");
   return JMT_OK;
 }

@@ -70,11 +70,14 @@ struct GemmParams {
 // PF: A-fragment prefetch distance in MFMA rows; PRIO: s_setprio(1) around each MFMA row;
 // SGB: sched_group_barrier pinning of each row's LDS reads ahead of its MFMAs.
 // OCC: minimum resident blocks per CU requested from the compiler (0: 2 x 256 threads' worth).
+// IL: the LDS-DMA of K-tile kt+S-1 is issued in pieces BETWEEN the MFMA rows of tile kt (per-lane
+// source offsets precomputed once per block, the K advance in scalar registers), instead of all
+// at once before the MFMAs: its issue overlaps the MFMA pipe (requires S >= 3).
 template <int BM_, int BN_, int WM_, int WN_, int KB_, int S_, int PF_ = 1, int PRIO_ = 0,
-          int SGB_ = 0, int OCC_ = 0>
+          int SGB_ = 0, int OCC_ = 0, int IL_ = 0>
 struct TileCfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, KB = KB_, S = S_;
-  static constexpr int PF = PF_, PRIO = PRIO_, SGB = SGB_;
+  static constexpr int PF = PF_, PRIO = PRIO_, SGB = SGB_, IL = IL_;
   static constexpr int OCC = OCC_ > 0 ? OCC_ : (2 * 256 / (64 * WM_ * WN_) > 0 ? 2 * 256 / (64 * WM_ * WN_) : 1);
   static constexpr int NT = 64 * WM * WN;          // threads per block
   static constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -93,6 +96,10 @@ using Cfg5 = TileCfg<256, 256, 2, 4, 128, 2, 1, 1, 0>;
 // block's epilogue and loads overlap the others' MFMAs; chosen by occupancy_override()
 using Cfg10 = TileCfg<128, 128, 2, 2, 64, 2, 1, 1, 0, 4>;
 using Cfg11 = TileCfg<128, 128, 2, 2, 64, 3, 1, 1, 0, 3>;
+// 256x256, 64-B K-tiles, 4 stages (3 tiles in flight), DMA issue interleaved with the MFMAs
+using Cfg20 = TileCfg<256, 256, 2, 4, 64, 4, 1, 1, 0, 0, 1>;
+// 128x128, 64-B K-tiles, 4 stages, interleaved issue, 2 blocks / CU
+using Cfg21 = TileCfg<128, 128, 2, 2, 64, 4, 1, 1, 0, 2, 1>;
 // (without s_setprio the two measured the same: profiles/r01_gemm_occupancy.txt)
 // (8-wave 128x256 / 256x128 tiles with 64-B K-tiles, 3 stages, 2 blocks / CU measured 20-100%
 // slower on every step shape: profiles/r01_gemm_occupancy.txt)
@@ -175,6 +182,42 @@ __device__ __forceinline__ void glds_tile(char* img, const T* base, int64_t ld, 
                                      (__attribute__((address_space(3))) void*)(img + q * 1024),
                                      16, 0, 0);
   }
+}
+
+// Interleaved staging (Cfg IL): the per-lane byte offset of each of this wave's LDS-DMA
+// instructions of one operand's K-tile, relative to the K-tile's scalar base (operand base +
+// k0 along K).  Constant over the K loop of a block: computed once.
+template <typename T, bool KMAJ, int KB, int ROWS, int NT>
+__device__ __forceinline__ void glds_offsets(uint32_t* off, int64_t ld, int rows_lim, int r0) {
+  constexpr int V = Vec<T>::n;
+  constexpr int NW = NT / 64;
+  constexpr int NI = ROWS * KB / 1024 / NW;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int q = w * NI + i;
+    int row, kk;
+    chunk_src<T, KMAJ, KB, ROWS>(q * 64 + lane, row, kk);
+    int64_t e;
+    if constexpr (KMAJ) {
+      e = (int64_t)min(r0 + row, rows_lim - 1) * ld + kk;
+    } else {
+      int gm = r0 + row;
+      if (gm >= rows_lim) gm = ((rows_lim - 1) / V) * V;
+      e = (int64_t)kk * ld + gm;
+    }
+    off[i] = (uint32_t)(e * (int64_t)sizeof(T));
+  }
+}
+
+// one LDS-DMA instruction i (this wave's slot) of an operand K-tile whose scalar base is `src`
+template <int NI>
+__device__ __forceinline__ void glds_slot(char* img, const char* src, const uint32_t* off, int i) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + off[i]),
+                                   (__attribute__((address_space(3))) void*)(img + (w * NI + i) * 1024),
+                                   16, 0, 0);
 }
 
 // Register staging of one (partial, masked) K-tile: NC chunks of 16 B per thread.
@@ -296,9 +339,14 @@ __device__ __forceinline__ void sgb_ds_reads(int n) {   // sched_group_barrier n
   }
 }
 
-template <typename T, bool AK, bool BK, class C>
+struct NoIssue {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+template <typename T, bool AK, bool BK, class C, class ISSUE = NoIssue>
 __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB, int wm, int wn,
-                                             f32x4 (&acc)[C::TM][C::TN]) {
+                                             f32x4 (&acc)[C::TM][C::TN],
+                                             const ISSUE& issue = ISSUE()) {
   if constexpr (sizeof(T) == 2) {
     // software-pipelined fragment reads: the A fragment of MFMA row i+1 (and, at the last row
     // of a k-step, the B fragments of the next k-step) are issued before the MFMAs of row i,
@@ -334,6 +382,7 @@ __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB,
                                                            r / C::TM);
         nreads += AK ? 1 : 2;
       }
+      issue(idx);                                   // interleaved LDS-DMA pieces (Cfg IL)
       if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < C::TN; ++j)
@@ -683,6 +732,60 @@ void gemm_kernel(GemmParams p) {
       if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
       __builtin_amdgcn_s_barrier();            // buffer (kt&1) free for tile kt+2
     }
+  } else if constexpr (C::IL) {
+    // S-1 tiles in flight, one barrier per tile; tile kt+S-1's DMA is issued in pieces between
+    // the MFMA rows of tile kt (buffer (kt-1) % S: freed by this iteration's barrier)
+    static_assert(C::S >= 3 && C::S <= 5, "interleaved staging needs 3-5 stages");
+    constexpr int NIA = C::BM * C::KB / 1024 / (C::NT / 64);
+    constexpr int NIB = C::BN * C::KB / 1024 / (C::NT / 64);
+    constexpr int NR = C::KB / 64 * C::TM;            // MFMA rows per K-tile
+    uint32_t offa[NIA], offb[NIB];
+    glds_offsets<T, AK, C::KB, C::BM, C::NT>(offa, p.lda, p.M, cur.m0);
+    glds_offsets<T, BK, C::KB, C::BN, C::NT>(offb, p.ldb, p.N, cur.n0);
+    auto bases = [&](int kt, const char*& sa, const char*& sb) {
+      const int k0 = cur.kbeg + kt * BKE;
+      int ka, kb;
+      const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, cur.b0, cur.b1, p.a_kseg, k0,
+                                   ka);
+      const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, cur.b0, cur.b1, p.b_kseg, k0,
+                                   kb);
+      sa = (const char*)(AK ? A + ka : A + (int64_t)ka * p.lda);
+      sb = (const char*)(BK ? B + kb : B + (int64_t)kb * p.ldb);
+    };
+#pragma unroll
+    for (int t = 0; t < C::S - 1; ++t)
+      if (t < nfull) {
+        const char *sa, *sb;
+        bases(t, sa, sb);
+        char* img = smem + t * C::STAGE;
+#pragma unroll
+        for (int i = 0; i < NIA; ++i) glds_slot<NIA>(img, sa, offa, i);
+#pragma unroll
+        for (int i = 0; i < NIB; ++i) glds_slot<NIB>(img + IA, sb, offb, i);
+      }
+    for (int kt = 0; kt < nfull; ++kt) {
+      wait_tiles<VMT>(min(C::S - 2, nfull - 1 - kt));
+      __builtin_amdgcn_s_barrier();
+      const int tn = kt + C::S - 1;
+      const char *sa = nullptr, *sb = nullptr;
+      char* nimg = smem + (tn % C::S) * C::STAGE;
+      if (tn < nfull) bases(tn, sa, sb);
+      const bool go = tn < nfull;
+      // piece q of the NIA + NIB instructions goes before MFMA row q * NR / (NIA + NIB)
+      auto issue = [&](int row) {
+        if (!go) return;
+#pragma unroll
+        for (int q = 0; q < NIA + NIB; ++q) {
+          if (row == q * NR / (NIA + NIB)) {
+            if (q < NIA) glds_slot<NIA>(nimg, sa, offa, q);
+            else glds_slot<NIB>(nimg + IA, sb, offb, q - NIA);
+          }
+        }
+      };
+      const char* img = smem + (kt % C::S) * C::STAGE;
+      if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc, issue);
+      else issue(0);
+    }
   } else {
     // S-1 tiles in flight, one barrier per tile: the barrier of iteration kt also certifies that
     // every wave finished computing tile kt-1, whose buffer receives tile kt+S-1.
@@ -808,6 +911,10 @@ static void launch_layout(const GemmParams& p, int cfg, dim3 grid, hipStream_t s
              [[fallthrough]];
     case 11: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg11>(p, grid, st); break; }
              [[fallthrough]];
+    case 20: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg20>(p, grid, st); break; }
+             [[fallthrough]];
+    case 21: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg21>(p, grid, st); break; }
+             [[fallthrough]];
     default: launch_cfg<T, O, AK, BK, Cfg1>(p, grid, st); break;
   }
 }
@@ -828,7 +935,7 @@ static void launch_t(const GemmParams& p, int ak, int bk, int cfg, dim3 grid, hi
 
 static void cfg_tile(int cfg, int& bm, int& bn) {
   switch (cfg) {
-    case 5: bm = 256; bn = 256; break;
+    case 5: case 20: bm = 256; bn = 256; break;
     default: bm = 128; bn = 128; break;
   }
 }
@@ -866,6 +973,9 @@ static bool tile_ok(const TileModel& t, int M, int N) {
 // Launch families where a 128x128 tile at 3-4 resident blocks / CU (Cfg10 / Cfg11) beat the
 // planner's choice by 3-11% in repeated step-shape sweeps (profiles/r01_gemm_occupancy.txt);
 // elsewhere they tie or lose, so they are selected by layout and shape, not by the cost model.
+// Round 2 (profiles/r02_gemm_step_shapes.txt, one process, cfg 0 / 5 / 20 / 21 interleaved):
+// the grouped NN dgrads run fastest on the interleaved-DMA 256x256 tile (Cfg20: -2..-18 %), the
+// grouped NT forwards on the plain 256x256 tile (-2..-7 % vs the round-1 128x128 overrides).
 static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, int splits) {
   if (!ak && !bk && M >= 1536 && N >= 512 && batch >= 3 && K >= 8192)
     return 10;                                                   // split-K qkv wgrad
@@ -873,9 +983,9 @@ static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, in
   if (!ak && !bk && batch >= 64 && M <= 512 && N <= 512 && K >= 128 && K <= 512)
     return 11;                                                   // attn dK / dV
   if (ak && !bk && batch == 1 && K >= 3072) return 11;           // K-concat stream dgrad
-  if (ak && !bk && batch >= 6 && K >= 1024 && K <= 2048 && M >= 4096) return 10;  // head dgrad
-  if (ak && bk && batch >= 3 && N >= 1536 && K == 512 && M >= 4096) return 11;   // grouped qkv
-  if (ak && !bk && batch == 6 && K == 512 && M >= 4096) return 11;    // cross-attn dgrad
+  if (ak && !bk && batch >= 3 && batch <= 8 && K >= 512 && M >= 4096 && N >= 512)
+    return 20;                                                   // grouped / head dgrads
+  if (ak && bk && batch >= 3 && K == 512 && M >= 4096 && N >= 512) return 5;   // grouped fwd
   return 0;
 }
 
@@ -1016,6 +1126,7 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
     int s_unused;
     plan(dt, d->M, d->N, d->K, batch0 * batch1, splits, cfg, s_unused);
     if (dt != JMT_F32 && (cfg == 1 || splits == 1)) {   // same 128x128 split plan when split
+      // (an override may pick a 256x256 tile: 5 or 20)
       const int t = occupancy_override(d->a_kmajor, d->b_kmajor, d->M, d->N, d->K,
                                        batch0 * batch1, splits);
       if (t) cfg = t;

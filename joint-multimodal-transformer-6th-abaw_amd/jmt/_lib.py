@@ -66,13 +66,13 @@ _PROTOS = {
     "jmt_softmax_bwd": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_i64, c_f, c_vp,
                                 c_i64, c_vp]),
     "jmt_attn_supported": (c_int, [c_int, c_int]),
-    "jmt_attn_mt_floats": (c_int, [c_int, c_int, c_int, c_int]),
     "jmt_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp,
                              c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_f, c_vp,
-                             c_vp, c_i64, c_vp, c_vp]),
-    "jmt_attn_bwd_dq": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
-                                c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
-                                c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_f, c_vp]),
+                             c_vp]),
+    "jmt_attn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp,
+                             c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                             c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_f, c_vp]),
+    "jmt_noop": (c_int, [c_vp]),
     "jmt_colsum_blocks": (c_int, [c_i64]),
     "jmt_colsum": (c_int, [c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_int, c_vp, c_vp]),
     "jmt_colsum_grouped": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_i64, c_vp, c_int,
@@ -120,7 +120,7 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.jmt_abi_version() != 2:
+    if lib.jmt_abi_version() != 3:
         raise JMTError("libjmt_hip.so ABI version mismatch")
     cfg = int(os.environ.get("JMT_GEMM_CFG", "0"))   # development: force a GEMM pipeline config
     if cfg:

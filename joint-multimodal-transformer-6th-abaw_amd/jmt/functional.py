@@ -20,6 +20,7 @@ from typing import Optional
 
 import torch
 from torch.autograd import Function
+from torch.autograd.function import once_differentiable
 
 from . import ops
 from . import streams
@@ -451,7 +452,9 @@ class AttnCoreFn(Function):
     q_src (Lq, N, *), k_src / v_src (Lk, N, *) in any strided seq-first layout, so self-attention
     (one packed qkv) and key-is-value cross-attention (q + packed kv) read their projections in
     place and write their gradients into packed buffers consumed by ONE in_proj dgrad/wgrad.
-    Scores are materialised as fp32 (N, H, Lq, ldS), probabilities in the compute dtype."""
+    16-bit head_dim 512: the fused kernels of attn.hip (no score matrix in the forward; the
+    backward recomputes P from lse).  Otherwise scores are materialised as fp32 (N, H, Lq, ldS),
+    probabilities in the compute dtype."""
 
     @staticmethod
     def _probs(q_src, k_src, E, H, qcol, kcol, ldS, scale, cd):
@@ -485,6 +488,7 @@ class AttnCoreFn(Function):
         return o
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, go):
         tensors = ctx.saved_tensors
         meta, owner = ctx.meta
@@ -517,18 +521,15 @@ def attn_forward(q_src, k_src, v_src, E, H, qcol, kcol, vcol):
     o = Rows(q_src).like(E, cd)
     fused = cd != torch.float32 and ops.attn_supported(_dc(cd), dh)
     if fused:
-        # one kernel: scores stay on chip (attn.hip); the unnormalised probabilities, the
-        # per-tile maxima and the lse are kept for the fused backward
+        # one kernel: scores stay on chip (attn.hip); only lse is kept for the backward, which
+        # recomputes the probabilities
         lse = torch.empty(N * H * Lq, dtype=torch.float32, device=dev)
-        P = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
-        mt = torch.empty(max(ops.attn_mt_floats(N, H, Lq, Lk), 1), dtype=torch.float32,
-                         device=dev)
         ops.attn_fwd(_dc(cd), N, H, Lq, Lk, dh,
                      _ptr(q_src, qcol), (q_src.stride(0), q_src.stride(1)),
                      _ptr(k_src, kcol), (k_src.stride(0), k_src.stride(1)),
                      _ptr(v_src, vcol), (v_src.stride(0), v_src.stride(1)),
-                     o.data_ptr(), (o.stride(0), o.stride(1)), scale, lse, P, ldS, mt)
-        tensors = (q_src, k_src, v_src, P, o, lse, mt)
+                     o.data_ptr(), (o.stride(0), o.stride(1)), scale, lse)
+        tensors = (q_src, k_src, v_src, None, o, lse)
     else:
         P = AttnCoreFn._probs(q_src, k_src, E, H, qcol, kcol, ldS, scale, cd)
         ops.gemm(M=Lq, N=dh, K=Lk, ab_dtype=_dc(cd), c_dtype=_dc(cd),
@@ -537,14 +538,14 @@ def attn_forward(q_src, k_src, v_src, E, H, qcol, kcol, vcol):
                  sB=(v_src.stride(1), dh),
                  c=[o.data_ptr()], ldc=o.stride(0), sC=(o.stride(1), dh),
                  batch0=N, batch1=H, device=dev)
-        tensors = (q_src, k_src, v_src, P, None, None, None)
+        tensors = (q_src, k_src, v_src, P, None, None)
     return o, (tensors, (E, H, qcol, kcol, vcol, ldS, scale, cd, fused))
 
 
 def attn_backward(saved, go, dq, dk, dv):
     """Gradients of attn_forward written into dq / dk / dv (seq-first views laid out like the
     sources; the same qcol/kcol/vcol column offsets; dq/dk/dv may be the same packed buffer)."""
-    (q_src, k_src, v_src, P, o, lse, mt), meta = saved
+    (q_src, k_src, v_src, P, o, lse), meta = saved
     E, H, qcol, kcol, vcol, ldS, scale, cd, fused = meta
     Lq, N = q_src.shape[0], q_src.shape[1]
     Lk = k_src.shape[0]
@@ -563,12 +564,14 @@ def attn_backward(saved, go, dq, dk, dv):
     bS = (H * Lq * ldS, Lq * ldS)
     dS = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
     if fused:
-        # dP, softmax backward and dQ = dS K in one kernel; P normalised in place
-        ops.attn_bwd_dq(_dc(cd), N, H, Lq, Lk, dh, go.data_ptr(), (so_l, so_n),
-                        o.data_ptr(), (o.stride(0), o.stride(1)),
-                        _ptr(k_src, kcol), (sk_l, sk_n), _ptr(v_src, vcol), (sv_l, sv_n),
-                        lse, P, mt, ldS, dS, _ptr(dq, qcol), (dq.stride(0), dq.stride(1)),
-                        scale)
+        # P recomputed from lse, dP, softmax backward and dQ = dS K in one kernel; the exact P
+        # and dS are written once for the dK / dV products below
+        P = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
+        ops.attn_bwd(_dc(cd), N, H, Lq, Lk, dh, go.data_ptr(), (so_l, so_n),
+                     o.data_ptr(), (o.stride(0), o.stride(1)),
+                     _ptr(q_src, qcol), (sq_l, sq_n), _ptr(k_src, kcol), (sk_l, sk_n),
+                     _ptr(v_src, vcol), (sv_l, sv_n), lse, P, dS, ldS,
+                     _ptr(dq, qcol), (dq.stride(0), dq.stride(1)), scale)
     else:
         dP = torch.empty(N * H * Lq * ldS, dtype=torch.float32, device=dev)
         ops.gemm(M=Lq, N=Lk, K=dh, ab_dtype=_dc(cd), c_dtype=F32,

@@ -101,9 +101,14 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
         d.ws_bytes = nbytes
     launch = lambda: _lib.check(_lib.load().jmt_gemm(C.byref(d), stream()), "jmt_gemm")
     if _launch_hook is not None:
-        _launch_hook({"ab_dtype": ab_dtype, "c_dtype": c_dtype, "a_kmajor": bool(a_kmajor),
-                      "b_kmajor": bool(b_kmajor), "M": M, "N": N, "K": K,
-                      "batch": batch0 * batch1, "beta": beta,
+        fam = {(True, True): "gemm_NT", (True, False): "gemm_NN", (False, False): "gemm_TN",
+               (False, True): "gemm_TT"}[(bool(a_kmajor), bool(b_kmajor))]
+        _launch_hook({"family": fam, "ab_dtype": ab_dtype, "c_dtype": c_dtype,
+                      "a_kmajor": bool(a_kmajor), "b_kmajor": bool(b_kmajor), "M": M, "N": N,
+                      "K": K, "batch": batch0 * batch1, "beta": beta,
+                      "flops": 2.0 * M * N * K * batch0 * batch1,
+                      "bytes": batch0 * batch1 * ((M + N) * K * (4 if ab_dtype == F32 else 2) +
+                                                  M * N * (4 if c_dtype == F32 else 2)),
                       "inplace": any(p in list(c) for p in list(a) + list(b))}, launch)
     else:
         launch()
@@ -158,27 +163,35 @@ def attn_supported(dtype: int, dh: int) -> bool:
     return _attn_fused["on"] and bool(_lib.load().jmt_attn_supported(dtype, dh))
 
 
-def attn_mt_floats(N, H, Lq, Lk) -> int:
-    return int(_lib.load().jmt_attn_mt_floats(N, H, Lq, Lk))
+def _hooked(info, launch):
+    if _launch_hook is not None:
+        return _launch_hook(info, launch)
+    return launch()
 
 
-def attn_fwd(dtype, N, H, Lq, Lk, dh, q_ptr, sq, k_ptr, sk, v_ptr, sv, o_ptr, so, scale, lse,
-             p=None, ldp=0, mt=None):
-    """Fused softmax(scale Q K^T) V; sq/sk/sv/so = (row stride, batch stride) in elements.
-    With p/mt (training) the unnormalised probabilities and per-tile maxima are kept for
-    attn_bwd_dq."""
-    _ptr = lambda t: t.data_ptr() if t is not None else None
-    _lib.call("jmt_attn_fwd", dtype, N, H, Lq, Lk, dh, q_ptr, sq[0], sq[1], k_ptr, sk[0], sk[1],
-              v_ptr, sv[0], sv[1], o_ptr, so[0], so[1], scale, _ptr(lse), _ptr(p), ldp, _ptr(mt),
-              stream())
+def noop():
+    _lib.call("jmt_noop", stream())
 
 
-def attn_bwd_dq(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, k_ptr, sk, v_ptr, sv, lse, p,
-                mt, ldp, ds, dq_ptr, sdq, scale):
-    """dS = scale P o (dO V^T - rowsum(dO o O)) and dQ = dS K; p normalised in place."""
-    _lib.call("jmt_attn_bwd_dq", dtype, N, H, Lq, Lk, dh, go_ptr, sgo[0], sgo[1], o_ptr, so[0],
-              so[1], k_ptr, sk[0], sk[1], v_ptr, sv[0], sv[1], lse.data_ptr(), p.data_ptr(),
-              mt.data_ptr(), ldp, ds.data_ptr(), dq_ptr, sdq[0], sdq[1], scale, stream())
+def attn_fwd(dtype, N, H, Lq, Lk, dh, q_ptr, sq, k_ptr, sk, v_ptr, sv, o_ptr, so, scale, lse):
+    """Fused softmax(scale Q K^T) V + lse; sq/sk/sv/so = (row stride, batch stride) in
+    elements."""
+    launch = lambda: _lib.call("jmt_attn_fwd", dtype, N, H, Lq, Lk, dh, q_ptr, sq[0], sq[1],
+                               k_ptr, sk[0], sk[1], v_ptr, sv[0], sv[1], o_ptr, so[0], so[1],
+                               scale, lse.data_ptr() if lse is not None else None, stream())
+    _hooked({"family": "attn_fwd", "flops": 4.0 * N * H * Lq * Lk * dh}, launch)
+
+
+def attn_bwd(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k_ptr, sk, v_ptr, sv,
+             lse, p, ds, ldp, dq_ptr, sdq, scale):
+    """P = exp(scale Q K^T - lse) and dS = scale P o (dO V^T - rowsum(dO o O)) written to p / ds
+    (ldp), dQ = dS K."""
+    launch = lambda: _lib.call("jmt_attn_bwd", dtype, N, H, Lq, Lk, dh, go_ptr, sgo[0], sgo[1],
+                               o_ptr, so[0], so[1], q_ptr, sq[0], sq[1], k_ptr, sk[0], sk[1],
+                               v_ptr, sv[0], sv[1], lse.data_ptr(), p.data_ptr(), ds.data_ptr(),
+                               ldp, dq_ptr, sdq[0], sdq[1], scale, stream())
+    # algorithmic: dP and dQ (the P recompute is not counted)
+    _hooked({"family": "attn_bwd", "flops": 4.0 * N * H * Lq * Lk * dh}, launch)
 
 
 def colsum(dy, ld, rows, N, db, beta_acc=False):

@@ -62,6 +62,47 @@ def test_gemm_layouts_dtypes(dt, ak, bk):
         assert torch.isnan(C[:, N:]).all(), "wrote outside N"
 
 
+@pytest.mark.parametrize("cfg", [1, 5, 10, 11, 20, 21])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_forced_configs(cfg, ak, bk):
+    """Every tile configuration of the planner forced on every operand layout (bf16), on ragged
+    shapes (partial tiles, trailing partial K-tile), a K-concatenated A and a pointer-table
+    batch: the interleaved-DMA configs (20, 21) keep three K-tiles in flight."""
+    from jmt import _lib
+    lib = _lib.load()
+    dt = BF16
+    g = torch.Generator(device=DEV).manual_seed(5)
+    lib.jmt_gemm_set_debug(cfg << 8)
+    try:
+        for (M, N, K) in [(300, 520, 512), (257, 129, 320), (64, 64, 1000), (1, 300, 96)]:
+            A, Al, lda, sa = _operand(M, K, ak, dt, batch=2, gen=g)
+            Bs, Bl_t, ldb, sb = _operand(N, K, bk, dt, batch=2, gen=g)
+            Bl = Bl_t.transpose(1, 2)
+            C = torch.full((2, M, N + 3), float("nan"), device=DEV)
+            ops.gemm(M=M, N=N, K=K, ab_dtype=dt, c_dtype=F32, a=[A.data_ptr()], lda=lda,
+                     a_kmajor=ak, sA=(sa, 0), b=[Bs[i].data_ptr() for i in range(2)], ldb=ldb,
+                     b_kmajor=bk, b_mode=1, c=[C.data_ptr()], ldc=N + 3, sC=(M * (N + 3), 0),
+                     batch0=2, splits=1, device=DEV)
+            for i in range(2):
+                ref = Al[i] @ Bl[i]
+                err = (C[i, :, :N] - ref).abs().max().item()
+                assert err <= _tol(dt, K) * max(1.0, ref.abs().max().item()), (cfg, M, N, K, err)
+            assert torch.isnan(C[:, :, N:]).all(), "wrote outside N"
+        if ak:   # K-concat A (3 segments of 128) x K-major / MN-major B, bf16 out
+            M, N, seg = 333, 256, 128
+            As = [torch.randn(M, seg, device=DEV, generator=g).bfloat16() for _ in range(3)]
+            Bs2, Bl_t2, ldb2, _ = _operand(N, 3 * seg, bk, dt, gen=g)
+            C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.gemm(M=M, N=N, K=3 * seg, ab_dtype=dt, c_dtype=dt, a=[a.data_ptr() for a in As],
+                     lda=seg, a_kmajor=True, a_mode=2, a_kseg=seg, b=[Bs2.data_ptr()], ldb=ldb2,
+                     b_kmajor=bk, c=[C.data_ptr()], ldc=N, splits=1, device=DEV)
+            ref = torch.cat([a.float() for a in As], 1) @ Bl_t2.transpose(1, 2)[0]
+            err = (C.float() - ref).abs().max().item()
+            assert err <= 1e-2 * ref.abs().max().item(), (cfg, "kcat", err)
+    finally:
+        lib.jmt_gemm_set_debug(0)
+
+
 @pytest.mark.parametrize("dt", [F32, BF16])
 def test_gemm_epilogues_and_splitk(dt):
     g = torch.Generator(device=DEV).manual_seed(2)
@@ -324,7 +365,7 @@ def test_sgd_matches_torch_nesterov():
 
 @pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("Lq,Lk,N", [(300, 300, 3), (1, 6, 40), (6, 6, 17), (70, 129, 2),
-                                     (64, 64, 1), (129, 1, 2)])
+                                     (64, 64, 1), (129, 1, 2), (1024, 1024, 2)])
 def test_fused_attention_fwd_vs_fp32(cd, Lq, Lk, N):
     """jmt_attn_fwd (attn.hip) on packed self/cross-attention layouts vs softmax(QK^T/sqrt(d))V
     in fp32 from the same rounded inputs; the log-sum-exp against torch.logsumexp."""
@@ -352,6 +393,87 @@ def test_fused_attention_fwd_vs_fp32(cd, Lq, Lk, N):
     assert err <= tol, err
     lref = torch.logsumexp(s, -1).reshape(-1)
     assert (lse - lref).abs().max().item() <= 1e-3 * max(lref.abs().max().item(), 1.0)
+
+
+@pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("Lq,Lk,N", [(300, 300, 3), (1, 6, 40), (70, 129, 2), (129, 1, 2),
+                                     (1024, 1024, 1)])
+def test_fused_attention_bwd_vs_fp32(cd, Lq, Lk, N):
+    """jmt_attn_bwd (attn.hip): P recomputed from the forward's lse, dS and dQ vs an fp32
+    reference from the same rounded inputs (P and dS are stored in the compute dtype; the
+    padding columns [Lk, ldp) of P and dS must be written as zeros)."""
+    E = 512
+    g = torch.Generator(device=DEV).manual_seed(23)
+    qkv = torch.randn(N, Lq, 3 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    kv = torch.randn(N, Lk, 2 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    qp, kp, vp = qkv[..., :E], kv[..., :E], kv[..., E:]
+    scale = 1.0 / math.sqrt(E)
+    dt = ops.dt(qkv)
+    o = torch.empty(Lq, N, E, device=DEV, dtype=cd)
+    lse = torch.empty(N * Lq, device=DEV, dtype=torch.float32)
+    ops.attn_fwd(dt, N, 1, Lq, Lk, E, qp.data_ptr(), (qkv.stride(0), qkv.stride(1)),
+                 kp.data_ptr(), (kv.stride(0), kv.stride(1)), vp.data_ptr(),
+                 (kv.stride(0), kv.stride(1)), o.data_ptr(), (o.stride(0), o.stride(1)), scale,
+                 lse)
+    go = torch.randn(Lq, N, E, device=DEV, generator=g).to(cd)
+    ldp = -(-Lk // 8) * 8
+    P = torch.full((N * Lq * ldp,), float("nan"), device=DEV, dtype=cd)
+    dS = torch.full((N * Lq * ldp,), float("nan"), device=DEV, dtype=cd)
+    dq = torch.full((N, Lq, 3 * E), float("nan"), device=DEV, dtype=cd).permute(1, 0, 2)
+    ops.attn_bwd(dt, N, 1, Lq, Lk, E, go.data_ptr(), (go.stride(0), go.stride(1)), o.data_ptr(),
+                 (o.stride(0), o.stride(1)), qp.data_ptr(), (qkv.stride(0), qkv.stride(1)),
+                 kp.data_ptr(), (kv.stride(0), kv.stride(1)), vp.data_ptr(),
+                 (kv.stride(0), kv.stride(1)), lse, P, dS, ldp, dq[..., E:2 * E].data_ptr(),
+                 (dq.stride(0), dq.stride(1)), scale)
+    torch.cuda.synchronize()
+    s = torch.einsum("lnd,knd->nlk", qp.float(), kp.float()) * scale
+    pr = torch.softmax(s, -1)
+    dp = torch.einsum("lnd,knd->nlk", go.float(), vp.float())
+    delta = (go.float() * o.float()).sum(-1).t().unsqueeze(-1)           # (N, Lq, 1)
+    dsr = pr * (dp - delta) * scale
+    dqr = torch.einsum("nlk,knd->lnd", dsr, kp.float())
+    Pg = P.view(N, Lq, ldp)
+    dSg = dS.view(N, Lq, ldp)
+    assert torch.isfinite(Pg.float()).all() and torch.isfinite(dSg.float()).all()
+    assert (Pg[..., Lk:] == 0).all() and (dSg[..., Lk:] == 0).all()
+    u = 2.0 ** -8 if cd == torch.bfloat16 else 2.0 ** -11
+    assert (Pg[..., :Lk].float() - pr).abs().max().item() <= 2 * u
+    # dS error floor: Delta = rowsum(dO o O) from the 16-bit O (the cancellation dP - Delta is
+    # exact zero at Lk = 1)
+    floor = 4 * u * scale * dp.abs().max().item()
+    e_ds = (dSg[..., :Lk].float() - dsr).abs().max().item()
+    assert e_ds <= 8 * u * dsr.abs().max().item() + floor, e_ds
+    e_dq = (dq[..., E:2 * E].float() - dqr).abs().max().item()
+    assert e_dq <= 16 * u * dqr.abs().max().item() + floor * kp.float().abs().max().item(), e_dq
+    assert torch.isnan(dq[..., :E].float()).all() and torch.isnan(dq[..., 2 * E:].float()).all()
+
+
+def test_fused_attention_forced_rescale():
+    """The lazy-rescale branch of the forward (a row max rising > 8 log2 units after the first
+    tile) must be exact: one key in the third 64-key tile is spiked to dominate one query row
+    (cdna_hip_programming.md §5.4 rule 26)."""
+    cd = torch.bfloat16
+    E, L, N = 512, 300, 2
+    g = torch.Generator(device=DEV).manual_seed(24)
+    q = torch.randn(N, L, E, device=DEV, generator=g) * 0.3
+    k = torch.randn(N, L, E, device=DEV, generator=g) * 0.3
+    v = torch.randn(N, L, E, device=DEV, generator=g)
+    k[0, 150] = q[0, 7] * 8.0           # tile 2 of row 7: score jump >> 8 (log2 units)
+    k[1, 299] = q[1, 63] * 8.0          # last (partial) tile
+    q, k, v = (t.to(cd).permute(1, 0, 2).contiguous() for t in (q, k, v))
+    o = torch.empty(L, N, E, device=DEV, dtype=cd)
+    lse = torch.empty(N * L, device=DEV, dtype=torch.float32)
+    scale = 1.0 / math.sqrt(E)
+    ops.attn_fwd(ops.dt(q), N, 1, L, L, E, q.data_ptr(), (q.stride(0), q.stride(1)),
+                 k.data_ptr(), (k.stride(0), k.stride(1)), v.data_ptr(), (v.stride(0), v.stride(1)),
+                 o.data_ptr(), (o.stride(0), o.stride(1)), scale, lse)
+    torch.cuda.synchronize()
+    s = torch.einsum("lnd,knd->nlk", q.float(), k.float()) * scale
+    ref = torch.einsum("nlk,knd->lnd", torch.softmax(s, -1), v.float())
+    assert (o.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    assert (o[7, 0].float() - v[150, 0].float()).abs().max().item() <= 2e-2
+    lref = torch.logsumexp(s, -1).reshape(-1)
+    assert (lse - lref).abs().max().item() <= 1e-3 * lref.abs().max().item()
 
 
 def test_fused_attention_matches_unfused_path():
