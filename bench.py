@@ -62,13 +62,22 @@ def step_flops(B: int, T: int, Da: int = D_A, Dv: int = D_V, fc: bool = True,
     """Algorithmic matmul FLOPs of one training step (SURVEY.md §8d closed form for
     TRANSFORMER/FC, L=1, h=d): F per window = input projections + out_layer_pv + 3 encoders +
     6 cross-attentions + out_layer1 + regressors; W = 3F minus the input gradients of the
-    projections that act on leaf inputs.  None for the other heads."""
-    if jm != "TRANSFORMER" or fmt != "FC":
+    projections that act on leaf inputs.  SELF_ATTEN swaps out_layer1 for its head.  None for
+    joint_modalities other than TRANSFORMER."""
+    if jm != "TRANSFORMER" or fmt not in ("FC", "SELF_ATTEN"):
         return None
     d = E
     proj = (2 * T * d * Da if fc else 0) + (2 * T * d * Dv if Dv != 512 else 0)
     F = (proj + 4 * T * d * d + 3 * (12 * T * d * d + 4 * T * T * d)
-         + 6 * (8 * T * d * d + 4 * T * T * d) + 24 * T * d * d + 4 * T * 1024 * 128 + 4 * T * 128)
+         + 6 * (8 * T * d * d + 4 * T * T * d) + 4 * T * 128)
+    if fmt == "FC":
+        F += 24 * T * d * d + 4 * T * 1024 * 128             # out_layer1 + regressors (1024)
+    else:
+        # SELF_ATTEN head (mm_multi_transformers.py:169-199): an encoder layer over the 6
+        # cross-attention outputs of every clip, then MHA with the last token as the only query
+        # row that is kept (q: 1 token, k/v: 6 tokens, out_proj: 1 token); regressors over 512
+        F += 6 * T * (12 * d * d + 4 * 6 * d) + T * (2 * d * d + 24 * d * d + 4 * 6 * d
+                                                    + 2 * d * d) + 4 * T * 512 * 128
     leaf = proj if proj else 4 * T * d * d + 2 * 6 * T * d * d
     return (3 * F - leaf) * B
 
@@ -89,6 +98,7 @@ class FamilyProbe:
         self.on = False
         self.rec = []
         self.cal = []
+        self.info = []
 
     @staticmethod
     def _pair(fn):
@@ -105,6 +115,7 @@ class FamilyProbe:
         from jmt import ops
         r, ev = self._pair(launch)
         self.rec.append((info["family"], info["flops"], info.get("bytes"), ev))
+        self.info.append({k: v for k, v in info.items() if isinstance(v, (int, float, str, bool))})
         _, e1 = self._pair(ops.noop)
         _, e2 = self._pair(lambda: (ops.noop(), ops.noop()))
         self.cal.append((e1, e2))
@@ -137,8 +148,26 @@ class FamilyProbe:
                         "gflop_per_launch": round(d["flops"] / d["launches"] / 1e9, 3),
                         "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
                         "tflops": round(tf, 1), "frac": round(tf / PEAK_BF16_TFLOPS, 4)})
+            if f.startswith("small_attn"):          # HBM-bound family: bytes, not flops
+                gbs = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+                out[-1].update({"bound": "hbm", "gbps": round(gbs, 1),
+                                "hbm_frac": round(gbs / PEAK_HBM_GBS, 4)})
         out.sort(key=lambda r: -r["ms_per_step"])
         return {"families": out, "event_pair_overhead_us": round(over * 1e3, 2)}
+
+    def dump(self, path: str, probe_steps: int):
+        """Per-launch records of the last probe step (shape, family, overhead-corrected us)."""
+        import statistics
+        ms = lambda ev: ev[0].elapsed_time(ev[1])
+        one = statistics.median(ms(a) for a, _ in self.cal)
+        two = statistics.median(ms(b) for _, b in self.cal)
+        over = max(0.0, one - (two - one))
+        n = len(self.rec) // probe_steps
+        with open(path, "w") as f:
+            for (fam, fl, by, ev), info in zip(self.rec[-n:], self.info[-n:]):
+                us = max(ms(ev) - over, 1e-6) * 1e3
+                info = dict(info, us=round(us, 2), tflops=round(fl / us / 1e6, 1))
+                f.write(json.dumps(info) + "\n")
 
 
 def parity_check(model, fc, audio, video, lv, la, cd, jm, fmt, Dv, nwin=2):
@@ -227,6 +256,7 @@ def main():
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="eager launches from Python every step")
     ap.add_argument("--probe-steps", type=int, default=3)
+    ap.add_argument("--launch-log", default=None, help="write per-launch records (jsonl)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -361,6 +391,8 @@ def main():
     value = windows / elapsed
 
     psum = probe.summary(args.probe_steps)
+    if args.launch_log and rank == 0 and probe.rec:
+        probe.dump(args.launch_log, args.probe_steps)
     roofline = None
     if psum:
         dom = psum["families"][0]                  # the family with the most in-step time

@@ -154,6 +154,26 @@ int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* go, i
                  void* ds_out, int64_t ldp, void* dq, int64_t sdq_l, int64_t sdq_n, float scale,
                  void* stream);
 
+/* Attention over short sequences (Lq, Lk <= 8; E = H*dh = 512, E/8/H a power of two, dt any of
+ * fp32/bf16/fp16): the SELF_ATTEN head's 6-token sequences (mm_multi_transformers.py:169-199)
+ * and intra-modal fusion's 2-token ones (intra_modal_transformer_fusion.py:93-108), same element
+ * addressing as jmt_attn_*, one wave per sequence n (HBM-bound; the 64-row fused kernels would
+ * idle >90 % of every tile). Rows 16-B aligned (32-B for fp32), strides multiples of 8.
+ * jmt_small_attn_fwd: o = softmax(scale Q K^T) V; if p_out != NULL the fp32 probabilities are
+ *   kept at p_out[((n*H + h)*Lq + l)*Lk + k] (N*H*Lq*Lk floats) for the backward.
+ * jmt_small_attn_bwd: dq = dS K, dk = dS^T Q, dv = P^T dO with dS = scale P o (dO V^T -
+ *   rowsum(P o dO V^T)); dq/dk/dv overwritten (they may be column slices of one buffer). */
+int jmt_small_attn_fwd(int dt, int N, int H, int Lq, int Lk, int E, const void* q, int64_t sq_l,
+                       int64_t sq_n, const void* k, int64_t sk_l, int64_t sk_n, const void* v,
+                       int64_t sv_l, int64_t sv_n, void* o, int64_t so_l, int64_t so_n,
+                       float scale, float* p_out, void* stream);
+int jmt_small_attn_bwd(int dt, int N, int H, int Lq, int Lk, int E, const void* go,
+                       int64_t sgo_l, int64_t sgo_n, const void* q, int64_t sq_l, int64_t sq_n,
+                       const void* k, int64_t sk_l, int64_t sk_n, const void* v, int64_t sv_l,
+                       int64_t sv_n, const float* p, void* dq, int64_t sdq_l, int64_t sdq_n,
+                       void* dk, int64_t sdk_l, int64_t sdk_n, void* dv, int64_t sdv_l,
+                       int64_t sdv_n, float scale, void* stream);
+
 /* Bias gradient: db[n] (+)= sum_m dy[m][n] (two-phase, deterministic, fp32 partial slabs of
  * jmt_colsum_blocks(rows) * N floats). */
 int jmt_colsum_blocks(int64_t rows);
@@ -166,12 +186,12 @@ int jmt_colsum_grouped(int dt, int G, int64_t rows, int N, const void* dy, int64
                        int64_t sdy, float* const* db_tab, int beta_acc, float* partials,
                        void* stream);
 
-/* Strided 2-D copy with dtype conversion and optional transpose (layout plumbing:
- * the (T,B) output of the FC head, torch.stack of the SELF_ATTEN head). dst may be accumulated
- * into (accumulate=1). */
 /* An empty one-block launch (measurement: the overhead of an event pair around a launch). */
 int jmt_noop(void* stream);
 
+/* Strided 2-D copy with dtype conversion and optional transpose (layout plumbing:
+ * the (T,B) output of the FC head, torch.stack of the SELF_ATTEN head). dst may be accumulated
+ * into (accumulate=1). */
 int jmt_copy2d(int src_dt, int dst_dt, int64_t rows, int64_t cols, const void* src,
                int64_t src_rs, int64_t src_cs, void* dst, int64_t dst_rs, int64_t dst_cs,
                int accumulate, void* stream);

@@ -73,6 +73,13 @@ _PROTOS = {
                              c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                              c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_f, c_vp]),
     "jmt_noop": (c_int, [c_vp]),
+    "jmt_small_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
+                                   c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
+                                   c_f, c_vp, c_vp]),
+    "jmt_small_attn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
+                                   c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
+                                   c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                   c_i64, c_f, c_vp]),
     "jmt_colsum_blocks": (c_int, [c_i64]),
     "jmt_colsum": (c_int, [c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_int, c_vp, c_vp]),
     "jmt_colsum_grouped": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_i64, c_vp, c_int,

@@ -497,12 +497,29 @@ class AttnCoreFn(Function):
         # one gradient buffer per distinct source tensor (packed qkv -> one buffer)
         srcs = (q_src, k_src, v_src)
         bufs = [None, None, None]
+        E, cols = meta[0], meta[2:5]
         for i in range(3):
             if owner[i] == i:
-                bufs[i] = Rows(srcs[i]).like(srcs[i].shape[-1], cd)
+                width = srcs[i].shape[-1]
+                bufs[i] = Rows(srcs[i]).like(width, cd)
+                # columns of a source that no Q/K/V slice reads get a zero gradient
+                covered = set()
+                for j in range(3):
+                    if owner[j] == i:
+                        covered.update(range(cols[j], cols[j] + E))
+                if len(covered) < width:
+                    bufs[i].zero_()
         attn_backward((tensors, meta), go, bufs[owner[0]], bufs[owner[1]], bufs[owner[2]])
         grads = [bufs[i] if owner[i] == i else None for i in range(3)]
         return (*grads, None, None, None, None, None)
+
+
+def _small_aligned(t, col, cd):
+    """Row starts 16-B (fp32: 32-B) aligned and strides multiples of 8 elements, as
+    jmt_small_attn_* require (include/jmt.h)."""
+    es = t.element_size()
+    return ((t.data_ptr() + col * es) % (32 if es == 4 else 16) == 0
+            and t.stride(0) % 8 == 0 and t.stride(1) % 8 == 0)
 
 
 def attn_forward(q_src, k_src, v_src, E, H, qcol, kcol, vcol):
@@ -519,8 +536,20 @@ def attn_forward(q_src, k_src, v_src, E, H, qcol, kcol, vcol):
     bS = (H * Lq * ldS, Lq * ldS)
     scale = 1.0 / math.sqrt(dh)
     o = Rows(q_src).like(E, cd)
-    fused = cd != torch.float32 and ops.attn_supported(_dc(cd), dh)
-    if fused:
+    small = ops.small_attn_ok(E, H, Lq, Lk) and all(
+        _small_aligned(t, c, cd) for t, c in ((q_src, qcol), (k_src, kcol), (v_src, vcol), (o, 0)))
+    fused = "small" if small else (cd != torch.float32 and ops.attn_supported(_dc(cd), dh))
+    if small:
+        # short sequences (SELF_ATTEN head, intra-modal fusion): one wave per sequence, the
+        # fp32 probabilities (N*H*Lq*Lk floats) kept for the backward (small_attn.hip)
+        P = torch.empty(N * H * Lq * Lk, dtype=torch.float32, device=dev)
+        ops.small_attn_fwd(_dc(cd), N, H, Lq, Lk, E,
+                           _ptr(q_src, qcol), (q_src.stride(0), q_src.stride(1)),
+                           _ptr(k_src, kcol), (k_src.stride(0), k_src.stride(1)),
+                           _ptr(v_src, vcol), (v_src.stride(0), v_src.stride(1)),
+                           o.data_ptr(), (o.stride(0), o.stride(1)), scale, P)
+        tensors = (q_src, k_src, v_src, P, None, None)
+    elif fused:
         # one kernel: scores stay on chip (attn.hip); only lse is kept for the backward, which
         # recomputes the probabilities
         lse = torch.empty(N * H * Lq, dtype=torch.float32, device=dev)
@@ -558,9 +587,17 @@ def attn_backward(saved, go, dq, dk, dv):
     sk_l, sk_n = k_src.stride(0), k_src.stride(1)
     sv_l, sv_n = v_src.stride(0), v_src.stride(1)
     so_l, so_n = go.stride(0), go.stride(1)
-    if fused and go.data_ptr() % 16:
+    if fused and not _small_aligned(go, 0, cd):
         go = go.clone(memory_format=torch.contiguous_format)
         so_l, so_n = go.stride(0), go.stride(1)
+    if fused == "small":
+        ops.small_attn_bwd(_dc(cd), N, H, Lq, Lk, E, go.data_ptr(), (so_l, so_n),
+                           _ptr(q_src, qcol), (sq_l, sq_n), _ptr(k_src, kcol), (sk_l, sk_n),
+                           _ptr(v_src, vcol), (sv_l, sv_n), P,
+                           _ptr(dq, qcol), (dq.stride(0), dq.stride(1)),
+                           _ptr(dk, kcol), (dk.stride(0), dk.stride(1)),
+                           _ptr(dv, vcol), (dv.stride(0), dv.stride(1)), scale)
+        return
     bS = (H * Lq * ldS, Lq * ldS)
     dS = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
     if fused:

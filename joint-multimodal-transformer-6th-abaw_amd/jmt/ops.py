@@ -194,6 +194,44 @@ def attn_bwd(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k_ptr, 
     _hooked({"family": "attn_bwd", "flops": 4.0 * N * H * Lq * Lk * dh}, launch)
 
 
+SMALL_ATTN_MAX_L = 8
+
+
+def small_attn_ok(E: int, H: int, Lq: int, Lk: int) -> bool:
+    """Shapes jmt_small_attn_* cover (include/jmt.h): E = 512, E/8/H a power of two, L <= 8
+    (off with the fused kernels: JMT_ATTN_FUSED=0 selects the GEMM + softmax path)."""
+    g = E // 8 // H if H > 0 and E % (8 * H) == 0 else 0
+    return (_attn_fused["on"] and E == 512 and g > 0 and (g & (g - 1)) == 0 and 1 <= Lq <= SMALL_ATTN_MAX_L
+            and 1 <= Lk <= SMALL_ATTN_MAX_L)
+
+
+def small_attn_fwd(dtype, N, H, Lq, Lk, E, q_ptr, sq, k_ptr, sk, v_ptr, sv, o_ptr, so, scale,
+                   p):
+    """O = softmax(scale Q K^T) V for Lq, Lk <= 8, one wave per sequence; p (fp32,
+    N*H*Lq*Lk) keeps the probabilities for small_attn_bwd."""
+    launch = lambda: _lib.call("jmt_small_attn_fwd", dtype, N, H, Lq, Lk, E, q_ptr, sq[0],
+                               sq[1], k_ptr, sk[0], sk[1], v_ptr, sv[0], sv[1], o_ptr, so[0],
+                               so[1], scale, p.data_ptr() if p is not None else None, stream())
+    es = 4 if dtype == F32 else 2
+    nbytes = float(N) * (2 * Lq + 2 * Lk) * E * es + (4.0 * N * H * Lq * Lk if p is not None
+                                                       else 0.0)
+    _hooked({"family": "small_attn_fwd", "flops": 4.0 * N * Lq * Lk * E, "bytes": nbytes},
+            launch)
+
+
+def small_attn_bwd(dtype, N, H, Lq, Lk, E, go_ptr, sgo, q_ptr, sq, k_ptr, sk, v_ptr, sv, p,
+                   dq_ptr, sdq, dk_ptr, sdk, dv_ptr, sdv, scale):
+    """dQ, dK, dV of small_attn_fwd from the kept P (no score recompute)."""
+    launch = lambda: _lib.call("jmt_small_attn_bwd", dtype, N, H, Lq, Lk, E, go_ptr, sgo[0],
+                               sgo[1], q_ptr, sq[0], sq[1], k_ptr, sk[0], sk[1], v_ptr, sv[0],
+                               sv[1], p.data_ptr(), dq_ptr, sdq[0], sdq[1], dk_ptr, sdk[0],
+                               sdk[1], dv_ptr, sdv[0], sdv[1], scale, stream())
+    es = 4 if dtype == F32 else 2
+    nbytes = float(N) * (3 * Lq + 4 * Lk) * E * es + 4.0 * N * H * Lq * Lk
+    _hooked({"family": "small_attn_bwd", "flops": 8.0 * N * Lq * Lk * E, "bytes": nbytes},
+            launch)
+
+
 def colsum(dy, ld, rows, N, db, beta_acc=False):
     nblk = _lib.load().jmt_colsum_blocks(rows)
     part = torch.empty(max(nblk, 1) * N, dtype=torch.float32, device=dy.device)

@@ -531,3 +531,113 @@ def test_colsum_grouped():
     for i in range(G):
         ref = i + dy[i].float().sum(0)
         assert (dbs[i] - ref).abs().max().item() < 1e-3
+
+
+def _small_ref(q, k, v, H, scale):
+    """fp32 softmax(scale Q K^T) V over (L, N, E) views; returns O (Lq, N, E) and P (N,H,Lq,Lk)."""
+    Lq, N, E = q.shape
+    Lk = k.shape[0]
+    dh = E // H
+    qh = q.reshape(Lq, N * H, dh).transpose(0, 1)
+    kh = k.reshape(Lk, N * H, dh).transpose(0, 1)
+    vh = v.reshape(Lk, N * H, dh).transpose(0, 1)
+    p = torch.softmax(scale * qh @ kh.transpose(1, 2), -1)
+    return (p @ vh).transpose(0, 1).reshape(Lq, N, E), p.reshape(N, H, Lq, Lk)
+
+
+@pytest.mark.parametrize("dt", [F32, BF16, F16])
+@pytest.mark.parametrize("H,Lq,Lk,N", [(1, 6, 6, 300), (1, 1, 6, 1000), (1, 2, 2, 77),
+                                       (1, 1, 2, 50), (8, 8, 8, 33), (8, 3, 5, 10), (1, 1, 1, 5),
+                                       (64, 4, 7, 9)])
+def test_small_attn_kernels_vs_fp32(dt, H, Lq, Lk, N):
+    """jmt_small_attn_fwd / _bwd (small_attn.hip) on q/k/v slices of packed projections in a
+    (N, L, *) memory layout (seq-first strided views, as the SELF_ATTEN head and intra-modal
+    fusion hand them over), against an fp32 torch reference on the same (16-bit-exact) inputs:
+    the kernels compute in fp32, so the only 16-bit error is the final rounding (<= 1 ulp)."""
+    cd = TD[dt]
+    E = 512
+    g = torch.Generator(device=DEV).manual_seed(100 + H + Lq * 8 + Lk)
+    pad = 64                                     # columns nobody may touch
+    if Lq == Lk:                                 # self-attention: one packed qkv
+        x = (2 * torch.randn(N, Lq, 3 * E + pad, device=DEV, generator=g)).to(cd)
+        qsrc, ksrc, vsrc, qc, kc, vc = x, x, x, 0, E, 2 * E
+    else:                                        # separate q, packed kv
+        qsrc = (2 * torch.randn(N, Lq, E + pad, device=DEV, generator=g)).to(cd)
+        ksrc = (2 * torch.randn(N, Lk, 2 * E + pad, device=DEV, generator=g)).to(cd)
+        vsrc, qc, kc, vc = ksrc, 0, 0, E
+    sf = lambda t: (t.stride(1), t.stride(0))    # (row stride, batch stride) of (N, L, *)
+    q = qsrc[..., qc:qc + E].permute(1, 0, 2)
+    k = ksrc[..., kc:kc + E].permute(1, 0, 2)
+    v = vsrc[..., vc:vc + E].permute(1, 0, 2)
+    scale = 1.0 / math.sqrt(E // H)
+    o = torch.full((N, Lq, E), float("nan"), dtype=cd, device=DEV)
+    P = torch.empty(N * H * Lq * Lk, dtype=torch.float32, device=DEV)
+    ops.small_attn_fwd(dt, N, H, Lq, Lk, E, q.data_ptr(), sf(qsrc), k.data_ptr(), sf(ksrc),
+                       v.data_ptr(), sf(vsrc), o.data_ptr(), sf(o), scale, P)
+    go = torch.randn(N, Lq, E, device=DEV, generator=g).to(cd)
+    gq = torch.full_like(qsrc, float("nan"))
+    gk = gq if ksrc is qsrc else torch.full_like(ksrc, float("nan"))
+    ops.small_attn_bwd(dt, N, H, Lq, Lk, E, go.data_ptr(), sf(go), q.data_ptr(), sf(qsrc),
+                       k.data_ptr(), sf(ksrc), v.data_ptr(), sf(vsrc), P,
+                       gq[..., qc:].data_ptr(), sf(gq), gk[..., kc:].data_ptr(), sf(gk),
+                       gk[..., vc:].data_ptr(), sf(gk), scale)
+    torch.cuda.synchronize()
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    ref, pref = _small_ref(qr, kr, vr, H, scale)
+    ref.backward(go.float().permute(1, 0, 2))
+    u = {F32: 2e-6, BF16: 2.0 ** -8, F16: 2.0 ** -11}[dt]
+    assert (P.view(N, H, Lq, Lk) - pref).abs().max().item() <= 2e-6
+    pairs = [(o.permute(1, 0, 2), ref), (gq[..., qc:qc + E].permute(1, 0, 2), qr.grad),
+             (gk[..., kc:kc + E].permute(1, 0, 2), kr.grad),
+             (gk[..., vc:vc + E].permute(1, 0, 2), vr.grad)]
+    for i, (got, want) in enumerate(pairs):
+        err = (got.float() - want).abs().max().item()
+        assert err <= 2 * u * want.abs().max().item() + 1e-6, (i, err)
+    # padding columns are never written
+    assert bool(torch.isnan(gq[..., -pad:]).all()) and bool(torch.isnan(gk[..., -pad:]).all())
+
+
+def test_small_attn_rejects_unsupported():
+    from jmt._lib import JMTError
+    x = torch.zeros(4, 9, 512, dtype=torch.bfloat16, device=DEV)
+    P = torch.empty(4 * 9 * 9, dtype=torch.float32, device=DEV)
+    args = (x.data_ptr(), (512, 9 * 512))
+    with pytest.raises(JMTError):                 # Lk = 9 > 8
+        ops.small_attn_fwd(BF16, 4, 1, 9, 9, 512, *args, *args, *args, *args, 1.0, P)
+    with pytest.raises(JMTError):                 # E != 512
+        ops.small_attn_fwd(BF16, 4, 1, 2, 2, 256, *args, *args, *args, *args, 1.0, P)
+    with pytest.raises(JMTError):                 # misaligned row start
+        ops.small_attn_fwd(BF16, 4, 1, 2, 2, 512, x.data_ptr() + 2, (512, 9 * 512), *args,
+                           *args, *args, 1.0, P)
+
+
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_short_sequences_dispatch_to_small_attn(cd):
+    """AttnCoreFn routes Lk <= 8 to the small kernels (SELF_ATTEN head shapes: packed qkv over 6
+    tokens, then the last-token query over them) and matches the GEMM + softmax path."""
+    fams = []
+    ops.set_launch_hook(lambda info, launch: (fams.append(info.get("family")), launch())[1])
+    g = torch.Generator(device=DEV).manual_seed(5)
+    N, E = 257, 512
+    x = torch.randn(N, 6, 3 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    outs = []
+    try:
+        for fused in (True, False):
+            ops._attn_fused["on"] = fused
+            fams.clear()
+            xx = x.detach().clone().requires_grad_(True)
+            with JF.compute_mode(cd):
+                o = JF.AttnCoreFn.apply(xx, xx, xx, E, 1, 0, E, 2 * E)
+                o2 = JF.AttnCoreFn.apply(o[-1:], xx, xx, E, 1, 0, E, 2 * E)
+            (o2.float().square().sum() + o.float().sum()).backward()
+            outs.append((o.float(), o2.float(), xx.grad.float()))
+            if fused:
+                assert fams.count("small_attn_fwd") == 2 and fams.count("small_attn_bwd") == 2
+            else:
+                assert "small_attn_fwd" not in fams
+    finally:
+        ops._attn_fused["on"] = True
+        ops.set_launch_hook(None)
+    tol = 1e-5 if cd == torch.float32 else 2e-2
+    for a, b in zip(*outs):
+        assert (a - b).abs().max().item() <= tol * b.abs().max().item()
