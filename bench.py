@@ -49,7 +49,9 @@ CONFIGS = {
     "c4": dict(B=16, T=1024, Da=1024, Dv=2048, fc=True, jm="TRANSFORMER", fmt="FC", dtype="bf16",
                desc="configs[3]: long window T=1024, TRANSFORMER/FC"),
     "c5": dict(B=128, T=300, Da=1024, Dv=2048, fc=True, jm="TRANSFORMER", fmt="FC", dtype="fp16",
-               desc="configs[4]: B=128 fp16 TRANSFORMER/FC"),
+               digitize=20,
+               desc="configs[4]: B=128 fp16 TRANSFORMER/FC, expression-style head: 20-bin V/A "
+                    "logits + losses.loss.CCCLoss(digitize_num=20) (loss.py:14-22)"),
     "realdata": dict(B=64, T=16, Da=512, Dv=512, fc=False, jm="TRANSFORMER", fmt="FC",
                      dtype="bf16", desc="shipped config_file.json: T=16 clips (512/32), R2D1 + "
                                         "ResNet18 features (512), Two_transformers(TRANSFORMER,"
@@ -58,7 +60,7 @@ CONFIGS = {
 
 
 def step_flops(B: int, T: int, Da: int = D_A, Dv: int = D_V, fc: bool = True,
-               jm: str = "TRANSFORMER", fmt: str = "FC"):
+               jm: str = "TRANSFORMER", fmt: str = "FC", k: int = 1):
     """Algorithmic matmul FLOPs of one training step (SURVEY.md §8d closed form for
     TRANSFORMER/FC, L=1, h=d): F per window = input projections + out_layer_pv + 3 encoders +
     6 cross-attentions + out_layer1 + regressors; W = 3F minus the input gradients of the
@@ -69,7 +71,7 @@ def step_flops(B: int, T: int, Da: int = D_A, Dv: int = D_V, fc: bool = True,
     d = E
     proj = (2 * T * d * Da if fc else 0) + (2 * T * d * Dv if Dv != 512 else 0)
     F = (proj + 4 * T * d * d + 3 * (12 * T * d * d + 4 * T * T * d)
-         + 6 * (8 * T * d * d + 4 * T * T * d) + 4 * T * 128)
+         + 6 * (8 * T * d * d + 4 * T * T * d) + 4 * T * 128 * k)
     if fmt == "FC":
         F += 24 * T * d * d + 4 * T * 1024 * 128             # out_layer1 + regressors (1024)
     else:
@@ -92,7 +94,9 @@ class FamilyProbe:
     launch is followed by two calibration pairs around empty launches (jmt_noop): one around a
     single empty launch, one around two back to back.  overhead = pair(1) - (pair(2) - pair(1))
     (the pair's fixed cost without the empty kernel's own execution) is subtracted from every
-    launch's reading."""
+    launch's reading.  Every pair is preceded by a GPU spin (torch.cuda._sleep), so the start
+    marker is stamped only after the host has queued the launch behind it: without it an
+    issue-bound step (small shapes, eager Python) puts the host's issue gap inside the pair."""
 
     def __init__(self):
         self.on = False
@@ -100,8 +104,13 @@ class FamilyProbe:
         self.cal = []
         self.info = []
 
+    SLEEP_CYCLES = 200000     # ~80 us spin ahead of each pair (torch.cuda._sleep)
+
     @staticmethod
     def _pair(fn):
+        # the GPU is kept busy while the host issues marker + launch + marker, so the pair
+        # times the kernel and not the host's issue latency (small launches are issue-bound)
+        torch.cuda._sleep(FamilyProbe.SLEEP_CYCLES)
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
@@ -170,31 +179,32 @@ class FamilyProbe:
                 f.write(json.dumps(info) + "\n")
 
 
-def parity_check(model, fc, audio, video, lv, la, cd, jm, fmt, Dv, nwin=2):
+def parity_check(model, fc, audio, video, lv, la, cd, jm, fmt, Dv, nwin=2, k=1, H=1, L=1):
     """BASELINE.json's '+ CCC parity': the GPU predictions and CCC losses in the compute dtype
     vs the CPU oracle (oracle/jmt_ref.py, fp32, pinned by the reference goldens) on the first
     `nwin` windows of the bench batch with the trained weights (north_star: 1e-2 bf16)."""
     from oracle import jmt_ref as R
     from jmt import functional as JF
     from losses.loss import CCCLoss
-    crit = CCCLoss(1)
+    crit = CCCLoss(k)
+    flat = (lambda o: o.reshape(-1, k)) if k > 1 else (lambda o: o.reshape(1, -1))
     a, v = audio[:nwin], video[:nwin]
     T = a.shape[1]
     yv = lv.view(audio.shape[0], T)[:nwin]
     ya = la.view(audio.shape[0], T)[:nwin]
     with torch.no_grad(), JF.compute_mode(cd):
         vo, ao = model(fc(a) if fc is not None else a, v)
-        gl1 = float(crit(vo.reshape(1, -1), yv.reshape(1, -1)))
-        gl2 = float(crit(ao.reshape(1, -1), ya.reshape(1, -1)))
+        gl1 = float(crit(flat(vo), yv.reshape(1, -1)))
+        gl2 = float(crit(flat(ao), ya.reshape(1, -1)))
     p = {k: t.detach().float().cpu() for k, t in model.state_dict().items()}
     with torch.no_grad():
         ac = a.float().cpu()
         if fc is not None:
             fp = {k: t.detach().float().cpu() for k, t in fc.state_dict().items()}
             ac = R.linear(ac, fp["fc_layer.weight"], fp["fc_layer.bias"])
-        rvo, rao = R.two_transformers_forward(ac, v.float().cpu(), p, 1, 1, jm, fmt, Dv)
-        rl1 = float(R.ccc_loss(rvo.reshape(1, -1), yv.cpu().reshape(1, -1)))
-        rl2 = float(R.ccc_loss(rao.reshape(1, -1), ya.cpu().reshape(1, -1)))
+        rvo, rao = R.two_transformers_forward(ac, v.float().cpu(), p, H, L, jm, fmt, Dv)
+        rl1 = float(R.ccc_loss(flat(rvo), yv.cpu().reshape(1, -1), digitize_num=k))
+        rl2 = float(R.ccc_loss(flat(rao), ya.cpu().reshape(1, -1), digitize_num=k))
     err = max(float((vo.float().cpu() - rvo).abs().max()), float((ao.float().cpu() - rao).abs().max()))
     lerr = max(abs(gl1 - rl1), abs(gl2 - rl2))
     return {"reference": "oracle/jmt_ref.py fp32 CPU, same weights (after the timed steps) and "
@@ -257,7 +267,18 @@ def main():
                     help="eager launches from Python every step")
     ap.add_argument("--probe-steps", type=int, default=3)
     ap.add_argument("--launch-log", default=None, help="write per-launch records (jsonl)")
-    args = ap.parse_args()
+    ap.add_argument("--config-file", default=None,
+                    help="a config_file.json (the reference's schema): model_params, the train "
+                         "batch / window and the opt__* SGD settings define the workload; further "
+                         "--key value pairs override it as parseit.py does (e.g. --num_heads 2 "
+                         "--opt__lr 1e-3 --train_params__batch_size 32)")
+    args, extra = ap.parse_known_args()
+    jcfg = None
+    if args.config_file:
+        from jmt import config as jconfig
+        jcfg = jconfig.override(jconfig.load(args.config_file), extra)
+    elif extra:
+        ap.error(f"unrecognized arguments: {' '.join(extra)}")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -284,15 +305,32 @@ def main():
     from models.fc_layer import FcLayer
     from losses.loss import CCCLoss
 
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    heads, layers, drop = 1, 1, (0.0, 0.0)
+    sgd_kw = dict(lr=1e-4, momentum=0.9, dampening=0.0, weight_decay=1e-4, nesterov=True)
+    if jcfg is not None:
+        # the shipped schema: R2D1 + ResNet18 features (512 each), no FcLayer (main.py:469-481)
+        mp = jcfg["model_params"]
+        jb, jt = jconfig.window(jcfg)
+        cfg = dict(B=jb, T=jt, Da=512, Dv=512, fc=False, jm=mp["joint_modalities"],
+                   fmt=mp["output_format"], dtype="bf16",
+                   desc=f"config file {os.path.basename(args.config_file)}"
+                        + (f" + {' '.join(extra)}" if extra else "")
+                        + f": T={jt} clips, batch {jb}, Two_transformers({mp['joint_modalities']},"
+                          f"{mp['output_format']},H={mp['num_heads']},L={mp['num_layers']})")
+        heads, layers = int(mp["num_heads"]), int(mp["num_layers"])
+        drop = (float(mp["v_dropout"]), float(mp["a_dropout"]))
+        sgd_kw = jconfig.sgd_kwargs(jcfg)
+    k = int(cfg.get("digitize", 1))
     args.dtype = args.dtype or cfg["dtype"]
     cd = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
     B = args.batch or cfg["B"]
     T = args.seq or cfg["T"]
     Da, Dv = cfg["Da"], cfg["Dv"]
-    fl_kw = dict(Da=Da, Dv=Dv, fc=cfg["fc"], jm=cfg["jm"], fmt=cfg["fmt"])
+    fl_kw = dict(Da=Da, Dv=Dv, fc=cfg["fc"], jm=cfg["jm"], fmt=cfg["fmt"], k=k)
     torch.manual_seed(0)
-    model = Two_transformers(0.0, 0.0, 1, 1, cfg["jm"], cfg["fmt"], Dv).to(dev)
+    model = Two_transformers(drop[0], drop[1], heads, layers, cfg["jm"], cfg["fmt"], Dv,
+                             digitize_num=k).to(dev)
     fc = FcLayer(Da, E).to(dev) if cfg["fc"] else None
     model_sd0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()} \
         if rank == 0 else None
@@ -307,7 +345,10 @@ def main():
     video = torch.randn(B, T, Dv, device=dev, generator=g)
     lv = (torch.rand(B, T, device=dev, generator=g) * 2 - 1).view(-1, B * T)
     la = (torch.rand(B, T, device=dev, generator=g) * 2 - 1).view(-1, B * T)
-    crit = CCCLoss(1)
+    crit = CCCLoss(k)
+    # k = 1: train.py:303-307's (1, T*B) views; k > 1 (c5's expression-style head): the (T, B, k)
+    # logits as the (N, k) rows loss.py:18-22 takes, labels (N,)
+    flat = (lambda o: o.reshape(-1, k)) if k > 1 else (lambda o: o.view(-1, o.shape[0] * o.shape[1]))
 
     # fp16 trains under loss scaling as the reference does (train.py:89,314-316); the scaler's
     # state lives on the device, so the step stays one graph replay
@@ -316,16 +357,15 @@ def main():
     def fwd_bwd():
         with JF.compute_mode(cd):
             vo, ao = model(fc(audio) if fc is not None else audio, video)
-            l1 = crit(vo.view(-1, vo.shape[0] * vo.shape[1]), lv)
-            l2 = crit(ao.view(-1, ao.shape[0] * ao.shape[1]), la)
+            l1 = crit(flat(vo), lv)
+            l2 = crit(flat(ao), la)
             loss = l1 + l2
             (scaler.scale(loss) if scaler is not None else loss).backward()
         return loss
 
     params = used_parameters(fwd_bwd, list(model.parameters()) +
                              (list(fc.parameters()) if fc is not None else []))
-    opt = FusedSGD(params, lr=1e-4, momentum=0.9, dampening=0.0, weight_decay=1e-4,
-                   nesterov=True, shadow_dtype=cd if cd != torch.float32 else None)
+    opt = FusedSGD(params, **sgd_kw, shadow_dtype=cd if cd != torch.float32 else None)
 
     def step():
         opt.zero_grad()
@@ -425,7 +465,8 @@ def main():
 
     parity = None
     if rank == 0 and not args.no_parity:
-        parity = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv)
+        parity = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv,
+                              k=k, H=heads, L=layers)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         cpu = cpu_baseline(model_sd0, fc_sd0, audio, video, lv, la)
@@ -438,7 +479,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.dtype, "data": "synthetic (N(0,1) features, U(-1,1) labels, "
                                          "random-init weights)",
-            "config": {"workload": cfg["desc"], "name": args.config,
+            "config": {"workload": cfg["desc"],
+                       "name": "config_file" if jcfg is not None else args.config,
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
                        "D_a": Da, "D_v": Dv, "parallelism": f"dp{world}",
                        "loss_scaling": "device GradScaler" if scaler is not None else None},

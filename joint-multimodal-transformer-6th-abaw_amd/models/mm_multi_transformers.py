@@ -32,7 +32,13 @@ class Attention(nn.Module):
         self.out_layer3 = Linear(64, 2)
 
     def forward(self, x):
-        raise NotImplementedError("dead code in the reference (never called)")
+        # mm_multi_transformers.py:19-26: additive attention weights over dim 1, then the
+        # 512 -> 256 -> 64 -> 2 projection chain (the linears on the HIP GEMM; tanh / softmax /
+        # the weighting are torch elementwise ops on this never-called path)
+        q = self.W(x)
+        attn_weights = torch.softmax(self.V(torch.tanh(q)), dim=1)
+        attended_x = attn_weights * x
+        return self.out_layer3(self.out_layer2(self.out_layer1(attended_x)))
 
 
 class SequentialEncoder(nn.Sequential):

@@ -22,7 +22,8 @@ class Two_transformers(nn.Module):
     (T, B) for TRANSFORMER/FC and (B, T) otherwise — the reference's layouts, reproduced."""
 
     def __init__(self, v_dropout: float, a_dropout: float, num_heads: int, num_layers: int,
-                 joint_modalities: str, output_format: str = 'FC', vision_in_ft: int = 512):
+                 joint_modalities: str, output_format: str = 'FC', vision_in_ft: int = 512,
+                 digitize_num: int = 1):
         super(Two_transformers, self).__init__()
         assert isinstance(v_dropout, float), type(v_dropout)
         assert 0.0 <= v_dropout < 1., v_dropout
@@ -67,8 +68,14 @@ class Two_transformers(nn.Module):
         else:
             raise NotImplementedError(joint_modalities)
 
-        self.vregressor = MLP(dim, 128, 1, dropout=v_dropout)
-        self.aregressor = MLP(dim, 128, 1, dropout=a_dropout)
+        # digitize_num = 1: the reference's V/A regressors (two_transformers.py:104-114).
+        # digitize_num = k > 1 (an extra keyword, default off): the same MLPs emit k bin logits
+        # per clip — the expression-style head SURVEY.md §8d maps configs[4] to, trained with
+        # losses.loss.CCCLoss(digitize_num=k) (loss.py:14-22) on the (N, k) rows
+        assert isinstance(digitize_num, int) and 1 <= digitize_num <= 64, digitize_num
+        self.digitize_num = digitize_num
+        self.vregressor = MLP(dim, 128, digitize_num, dropout=v_dropout)
+        self.aregressor = MLP(dim, 128, digitize_num, dropout=a_dropout)
 
     def forward(self, f1_norm, f2_norm):
         video = F.l2_normalize(f2_norm)          # :118
@@ -81,7 +88,7 @@ class Two_transformers(nn.Module):
         # regressors in fp32 out (predictions feed the fp32 CCC statistics)
         vouts = self.vregressor(av, out_dtype=torch.float32).squeeze(2)
         aouts = self.aregressor(av, out_dtype=torch.float32).squeeze(2)
-        if not vouts.is_contiguous():             # seq-first (T,B) views -> contiguous (T,B)
+        if vouts.dim() == 2 and not vouts.is_contiguous():   # seq-first (T,B) -> contiguous
             vouts = F.TransposeCopyFn.apply(vouts)
             aouts = F.TransposeCopyFn.apply(aouts)
         return vouts, aouts

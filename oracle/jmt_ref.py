@@ -397,7 +397,7 @@ def _block_shapes(pre: str, E: int, Hd: int, L: int) -> dict:
 
 
 def two_transformers_shapes(L: int, joint_modalities: str, output_format: str = "FC",
-                            vision_in_ft: int = 512) -> dict:
+                            vision_in_ft: int = 512, digitize_num: int = 1) -> dict:
     """state_dict key -> shape of Two_transformers (SURVEY.md §8a 'state_dict keys')."""
     d = {}
     if vision_in_ft != 512:
@@ -430,7 +430,7 @@ def two_transformers_shapes(L: int, joint_modalities: str, output_format: str = 
         dim = 512
     for r in ("vregressor.", "aregressor."):
         d.update({r + "0.weight": (128, dim), r + "0.bias": (128,),
-                  r + "3.weight": (1, 128), r + "3.bias": (1,)})
+                  r + "3.weight": (digitize_num, 128), r + "3.bias": (digitize_num,)})
     return d
 
 

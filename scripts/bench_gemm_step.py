@@ -17,22 +17,26 @@ from jmt._lib import BF16, F32  # noqa: E402
 
 R = 19200
 # name, M, N, K, a_kmajor, b_kmajor, batch, c_dtype, extra
-SHAPES = [
-    ("enc b3 fwd NT 512x512", R, 512, 512, True, True, 3, BF16, {}),
-    ("enc b3 qkv NT 1536x512", R, 1536, 512, True, True, 3, BF16, {}),
-    ("enc b3 dgrad NN 512x512", R, 512, 512, True, False, 3, BF16, {}),
-    ("enc b3 dgrad NN beta", R, 512, 512, True, False, 3, BF16, {"beta": 1.0}),
-    ("enc b3 dgrad NN aux", R, 512, 512, True, False, 3, BF16, {"aux": True}),
-    ("enc b3 dgrad NN K1536 beta", R, 512, 1536, True, False, 3, BF16, {"beta": 1.0}),
-    ("ca b6 dgrad NN 512x512", R, 512, 512, True, False, 6, BF16, {}),
-    ("ca b6 kv NT 1024x512", R, 1024, 512, True, True, 6, BF16, {}),
-    ("stream dgrad kcat6 NN 512x3072", R, 512, 3072, True, False, 1, BF16, {"kcat": 6}),
-    ("head dgrad b6 NN 512x1024", R, 512, 1024, True, False, 6, BF16, {"sA0": True}),
-    ("head fwd kcat6 NT 1024x3072", R, 1024, 3072, True, True, 1, BF16, {"kcat": 6}),
-    ("wgrad b3 TN 512x512xR", 512, 512, R, False, False, 3, F32, {"beta": 1.0}),
-    ("wgrad b3 TN 1536x512xR", 1536, 512, R, False, False, 3, F32, {"beta": 1.0}),
-    ("attn dKdV b384 TN 300x512x300", 300, 512, 300, False, False, 384, BF16, {}),
-]
+def make_shapes(R):
+    return [
+        ("enc b3 fwd NT 512x512", R, 512, 512, True, True, 3, BF16, {}),
+        ("enc b3 qkv NT 1536x512", R, 1536, 512, True, True, 3, BF16, {}),
+        ("enc b3 dgrad NN 512x512", R, 512, 512, True, False, 3, BF16, {}),
+        ("enc b3 dgrad NN beta", R, 512, 512, True, False, 3, BF16, {"beta": 1.0}),
+        ("enc b3 dgrad NN aux", R, 512, 512, True, False, 3, BF16, {"aux": True}),
+        ("enc b3 dgrad NN K1536 beta", R, 512, 1536, True, False, 3, BF16, {"beta": 1.0}),
+        ("ca b6 dgrad NN 512x512", R, 512, 512, True, False, 6, BF16, {}),
+        ("ca b6 kv NT 1024x512", R, 1024, 512, True, True, 6, BF16, {}),
+        ("stream dgrad kcat6 NN 512x3072", R, 512, 3072, True, False, 1, BF16, {"kcat": 6}),
+        ("head dgrad b6 NN 512x1024", R, 512, 1024, True, False, 6, BF16, {"sA0": True}),
+        ("head fwd kcat6 NT 1024x3072", R, 1024, 3072, True, True, 1, BF16, {"kcat": 6}),
+        ("wgrad b3 TN 512x512xR", 512, 512, R, False, False, 3, F32, {"beta": 1.0}),
+        ("wgrad b3 TN 1536x512xR", 1536, 512, R, False, False, 3, F32, {"beta": 1.0}),
+        ("attn dKdV b384 TN 300x512x300", 300, 512, 300, False, False, 384, BF16, {}),
+    ]
+
+
+SHAPES = make_shapes(R)
 
 
 def run(reps, cfg, dbg=0):
@@ -89,7 +93,9 @@ if __name__ == "__main__":
     ap.add_argument("--cfg", type=int, nargs="*", default=[0])
     ap.add_argument("--only", default="")
     ap.add_argument("--dbg", type=int, nargs="*", default=[0])
+    ap.add_argument("--rows", type=int, default=R, help="tokens per stream (realdata: 1024)")
     args = ap.parse_args()
+    SHAPES[:] = make_shapes(args.rows)
     if args.only:
         SHAPES[:] = [s for s in SHAPES if args.only in s[0]]
     for c in args.cfg:

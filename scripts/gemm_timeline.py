@@ -20,8 +20,9 @@ from jmt import _lib  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--only", default="fwd NT 512")
 ap.add_argument("--cfg", type=int, nargs="*", default=[5])
+ap.add_argument("--rows", type=int, default=B.R)
 args = ap.parse_args()
-B.SHAPES[:] = [s for s in B.SHAPES if args.only in s[0]]
+B.SHAPES[:] = [s for s in B.make_shapes(args.rows) if args.only in s[0]]
 lib = _lib.load()
 for cfg in args.cfg:
     B.run(3, cfg, 8)      # last launch leaves its stamps

@@ -127,3 +127,62 @@ def test_config_shapes_vs_oracle(cfg, cd):
         e_emu = float((emu - ref).abs().max())
         assert e_gpu <= K16 * max(e_emu, UNIT[cd] * spread), (e_gpu, e_emu)
     assert abs(loss - rloss) <= K16 * max(abs(eloss - rloss), UNIT[cd]), (loss, rloss, eloss)
+
+
+def test_c5_expression_head_fp16_vs_oracle():
+    """configs[4]'s expression-style head: the V/A MLPs emit k = 20 bin logits and
+    losses.loss.CCCLoss(digitize_num=20) (loss.py:14-22: softmax over the bins, expectation over
+    linspace(-1, 1, 20), CCC) trains them, in fp16 with loss scaling (1024, as GradScaler) — logits,
+    loss and the head's gradients vs the fp32 oracle within the fp16 error model."""
+    from losses.loss import CCCLoss
+    from models.two_transformers import Two_transformers
+    from models.fc_layer import FcLayer
+    from oracle.hashinit import features, labels
+    torch.set_num_threads(16)
+    k, B, T, cd = 20, 2, 300, torch.float16
+    m = Two_transformers(0.0, 0.0, 1, 1, "TRANSFORMER", "FC", 2048, digitize_num=k)
+    fc = FcLayer(1024, E)
+    init_module_(m, "")
+    init_module_(fc, "fc.")
+    m, fc = m.to(DEV), fc.to(DEV)
+    audio = torch.from_numpy(features("c5.audio", (B, T, 1024)))
+    video = torch.from_numpy(features("c5.video", (B, T, 2048)))
+    lv = torch.from_numpy(labels("c5.lv", (B, T)))
+    la = torch.from_numpy(labels("c5.la", (B, T)))
+    crit = CCCLoss(k)
+    with JF.compute_mode(cd):
+        vo, ao = m(fc(audio.to(DEV)), video.to(DEV))
+        assert vo.shape == (T, B, k)
+        loss = crit(vo.reshape(-1, k), lv.to(DEV).view(1, -1)) + \
+            crit(ao.reshape(-1, k), la.to(DEV).view(1, -1))
+        (loss * 1024.0).backward()
+    names = ["vregressor.3.weight", "vregressor.0.weight", "aregressor.3.weight"]
+    gpu_g = {n: dict(m.named_parameters())[n].grad.float().cpu() / 1024.0 for n in names}
+    p, fp = _state(m, fc)
+
+    def oracle(emulate):
+        pp = {n: t.clone().requires_grad_(True) for n, t in p.items()}
+        import contextlib
+        ctx = R.emulate_storage(cd) if emulate else contextlib.nullcontext()
+        with ctx:
+            aud = R.linear(audio, fp["fc_layer.weight"], fp["fc_layer.bias"])
+            rvo, rao = R.two_transformers_forward(aud, video, pp, 1, 1, "TRANSFORMER", "FC", 2048)
+            rl = R.ccc_loss(rvo.reshape(-1, k), lv.reshape(1, -1), digitize_num=k) + \
+                R.ccc_loss(rao.reshape(-1, k), la.reshape(1, -1), digitize_num=k)
+            rl.backward()
+        return rvo.detach(), rao.detach(), float(rl), {n: pp[n].grad for n in names}
+
+    rvo, rao, rl, rg = oracle(False)
+    evo, eao, el, eg = oracle(True)
+    spread = float(max(rvo.max() - rvo.min(), rao.max() - rao.min()))
+    assert spread > 0.1, spread
+    for got, emu, ref in ((vo.detach().float().cpu(), evo, rvo), (ao.detach().float().cpu(), eao, rao)):
+        e_gpu = float((got - ref).abs().max())
+        e_emu = float((emu - ref).abs().max())
+        assert e_gpu <= K16 * max(e_emu, UNIT[cd] * spread), (e_gpu, e_emu)
+    assert abs(float(loss) - rl) <= K16 * max(abs(el - rl), UNIT[cd]), (float(loss), rl, el)
+    for n in names:
+        nrm = float(rg[n].norm())
+        e_gpu = float((gpu_g[n] - rg[n]).norm()) / nrm
+        e_emu = float((eg[n] - rg[n]).norm()) / nrm
+        assert e_gpu <= K16 * max(e_emu, 2 * UNIT[cd]), (n, e_gpu, e_emu)

@@ -1,0 +1,224 @@
+"""Data parallelism through the PRODUCT path: two ranks sharing cuda:0 over gloo,
+each running the HIP drop-ins on its contiguous batch shard (jmt.dist.shard_range), the
+reference's losses with the process group registered (jmt.dist.set_loss_group: the CCC
+statistics all-gathered, the global-batch CCC on every rank) and the gradients summed over one
+flat buffer (jmt.dist.FlatGrads) — against the DataParallel semantics the reference trains with
+(main.py:487-491: replicas on dim-0 shards, outputs gathered on dim 0; train.py:303-311: the loss
+on the gathered batch), restated on the CPU oracle (oracle/jmt_ref.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B, T, VIN = 4, 16, 512
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs():
+    from oracle.hashinit import features, labels
+    return (torch.from_numpy(features("dp.audio", (B, T, 512))),
+            torch.from_numpy(features("dp.video", (B, T, VIN))),
+            torch.from_numpy(labels("dp.lv", (B, T))), torch.from_numpy(labels("dp.la", (B, T))))
+
+
+def _model():
+    from models.two_transformers import Two_transformers
+    from oracle.hashinit import init_module_
+    m = Two_transformers(0.0, 0.0, 1, 1, "TRANSFORMER", "FC", VIN)
+    init_module_(m, "")
+    return m
+
+
+def _spawn(target, args, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for p in procs:
+        assert p.exitcode == 0, p.exitcode
+    return out
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    torch.set_num_threads(2)
+    from jmt import dist as jdist
+    jdist.set_loss_group(dist.group.WORLD)
+    return dist, jdist
+
+
+def _train_step_worker(rank, world, port, q, cd_name):
+    dist, jdist = _init(rank, world, port)
+    try:
+        from jmt import functional as JF
+        from losses.loss import CCCLoss
+        cd = getattr(torch, cd_name)
+        audio, video, lv, la = _inputs()
+        lo, hi = jdist.shard_range(B, rank, world)
+        m = _model().cuda()
+        fg = jdist.FlatGrads(list(m.parameters()), "cuda")
+        fg.zero_()
+        crit = CCCLoss(1)
+        with JF.compute_mode(cd):
+            vo, ao = m(audio[lo:hi].cuda(), video[lo:hi].cuda())
+            # train.py:303-307 on the replica's (T, b) outputs and the shard's (b, T) labels
+            vout = vo.view(-1, vo.shape[0] * vo.shape[1])
+            aout = ao.view(-1, ao.shape[0] * ao.shape[1])
+            n = (hi - lo) * T
+            loss = crit(vout, lv[lo:hi].cuda().view(-1, n)) + crit(aout, la[lo:hi].cuda().view(-1, n))
+            loss.backward()
+        fg.allreduce_()
+        torch.cuda.synchronize()
+        grads = {k: p.grad.detach().float().cpu().numpy() for k, p in m.named_parameters()
+                 if p.grad is not None}
+        q.put((rank, float(loss), grads))
+    finally:
+        dist.destroy_process_group()
+
+
+def _dp_oracle():
+    """nn.DataParallel on 2 replicas, restated on the CPU oracle: per-replica forward on the
+    dim-0 shard, outputs gathered on dim 0, CCC on the gathered (1, B*T) view, grads."""
+    from oracle import jmt_ref as R
+    m = _model()
+    p = {k: v.detach().clone().float().requires_grad_(True) for k, v in m.state_dict().items()}
+    audio, video, lv, la = _inputs()
+    vos, aos = [], []
+    for r in range(2):
+        sl = slice(r * B // 2, (r + 1) * B // 2)
+        vo, ao = R.two_transformers_forward(audio[sl], video[sl], p, 1, 1, "TRANSFORMER", "FC",
+                                            VIN)
+        vos.append(vo)
+        aos.append(ao)
+    vo, ao = torch.cat(vos, 0), torch.cat(aos, 0)
+    loss = R.ccc_loss(vo.reshape(1, -1), lv.reshape(1, -1)) + \
+        R.ccc_loss(ao.reshape(1, -1), la.reshape(1, -1))
+    loss.backward()
+    return float(loss), {k: t.grad for k, t in p.items() if t.grad is not None}
+
+
+def _single_gpu(cd):
+    """The same full batch in ONE process (the 1-GPU product path)."""
+    from jmt import functional as JF
+    from losses.loss import CCCLoss
+    audio, video, lv, la = _inputs()
+    m = _model().cuda()
+    crit = CCCLoss(1)
+    with JF.compute_mode(cd):
+        vo, ao = m(audio.cuda(), video.cuda())
+        loss = crit(vo.reshape(1, -1), lv.cuda().view(1, -1)) + \
+            crit(ao.reshape(1, -1), la.cuda().view(1, -1))
+        loss.backward()
+    return float(loss), {k: p.grad.detach().float().cpu() for k, p in m.named_parameters()
+                         if p.grad is not None}
+
+
+def test_two_rank_product_path_fp32_matches_dataparallel_oracle():
+    out = _spawn(_train_step_worker, ("float32",))
+    ref_loss, ref_grads = _dp_oracle()
+    gmax = max(float(g.abs().max()) for g in ref_grads.values())
+    (_, l0, g0), (_, l1, g1) = out
+    assert l0 == l1, (l0, l1)                                  # global-batch loss on every rank
+    assert abs(l0 - ref_loss) <= 1e-5, (l0, ref_loss)
+    assert set(ref_grads) <= set(g0), set(ref_grads) - set(g0)
+    for k in g0:
+        assert np.array_equal(g0[k], g1[k]), k                 # all-reduced: identical replicas
+        if k not in ref_grads:                                 # never used by the forward
+            assert not g0[k].any(), k                          # (final_encoder): zero in FlatGrads
+            continue
+        r = ref_grads[k]
+        err = float((torch.from_numpy(g0[k]) - r).abs().max())
+        assert err <= 1e-4 * max(float(r.abs().max()), 0.01 * gmax), (k, err)
+
+
+def test_two_rank_product_path_bf16_matches_single_gpu():
+    """bf16: the 2-rank run equals the one-process full-batch run up to the summation order of
+    the per-rank gradient halves (the per-window forward does not depend on the batch split)."""
+    out = _spawn(_train_step_worker, ("bfloat16",))
+    ref_loss, ref_grads = _single_gpu(torch.bfloat16)
+    gmax = max(float(g.abs().max()) for g in ref_grads.values())
+    (_, l0, g0), (_, l1, g1) = out
+    assert l0 == l1
+    assert abs(l0 - ref_loss) <= 1e-4, (l0, ref_loss)
+    for k in ref_grads:
+        r = ref_grads[k]
+        err = float((torch.from_numpy(g0[k]) - r).abs().max())
+        assert err <= 2e-2 * max(float(r.abs().max()), 0.01 * gmax), (k, err)
+
+
+SIZES = (7, 12)     # unequal per-rank batches
+
+
+def _loss_worker(rank, world, port, q, kind):
+    dist, jdist = _init(rank, world, port)
+    try:
+        from oracle.hashinit import features, labels
+        n = SIZES[rank]
+        off = sum(SIZES[:rank])
+        tot = sum(SIZES)
+        if kind == "ignore":
+            from losses.CCCLoss import CCCLoss
+            x = torch.from_numpy(features("dpl.x", (tot,)))[off:off + n]
+            y = torch.from_numpy(labels("dpl.y", (tot,), ignore_frac=0.3))[off:off + n]
+            crit = CCCLoss(-5.0)
+        else:                               # digitized expectation CCC, k = 5 bins
+            from losses.loss import CCCLoss
+            x = torch.from_numpy(features("dpl.logits", (tot, 5)))[off:off + n] * 3
+            y = torch.from_numpy(labels("dpl.y5", (tot,)))[off:off + n].view(1, -1)
+            crit = CCCLoss(5)
+        xg = x.cuda().requires_grad_(True)
+        loss = crit(xg, y.cuda())
+        loss.backward()
+        torch.cuda.synchronize()
+        q.put((rank, float(loss), xg.grad.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["ignore", "digitized"])
+def test_two_rank_losses_unequal_shards_match_gathered_batch(kind):
+    """losses/CCCLoss.py (ignore-masked, 1-D: the gathered size(0) is the SUM of the ranks'
+    sizes) and losses/loss.py CCCLoss(digitize_num=5) on 7 + 12 elements: every rank's loss
+    equals the loss of the gathered batch and its gradient the matching slice of that loss's."""
+    from oracle import jmt_ref as R
+    from oracle.hashinit import features, labels
+    out = _spawn(_loss_worker, (kind,))
+    tot = sum(SIZES)
+    if kind == "ignore":
+        x = torch.from_numpy(features("dpl.x", (tot,))).double().requires_grad_(True)
+        y = torch.from_numpy(labels("dpl.y", (tot,), ignore_frac=0.3)).double()
+        ref = R.ccc_loss_ignore(x, y, -5.0)
+    else:
+        x = (torch.from_numpy(features("dpl.logits", (tot, 5))) * 3).double().requires_grad_(True)
+        y = torch.from_numpy(labels("dpl.y5", (tot,))).double()
+        ref = R.ccc_loss(x, y.view(1, -1), digitize_num=5)
+    ref.backward()
+    off = 0
+    for rank, loss, g in out:
+        assert abs(loss - float(ref)) <= 1e-5, (rank, loss, float(ref))
+        gr = x.grad[off:off + SIZES[rank]].numpy()
+        assert np.abs(g - gr).max() <= 1e-5 * max(1.0, np.abs(gr).max()), (rank, g, gr)
+        off += SIZES[rank]

@@ -47,8 +47,12 @@ def test_constructor_signatures_match_reference():
     from losses.loss import CCCLoss, CELoss, CCC_CE_Loss
     from losses.CCCLoss import CCCLoss as CCCLossIgnore
     sig = lambda c: list(inspect.signature(c.__init__).parameters)[1:]
+    # the reference's positional parameters in order; the one extra (digitize_num: configs[4]'s
+    # expression-style head) comes after them with a default that keeps the reference behaviour
     assert sig(Two_transformers) == ["v_dropout", "a_dropout", "num_heads", "num_layers",
-                                     "joint_modalities", "output_format", "vision_in_ft"]
+                                     "joint_modalities", "output_format", "vision_in_ft",
+                                     "digitize_num"]
+    assert inspect.signature(Two_transformers.__init__).parameters["digitize_num"].default == 1
     assert sig(MultimodalTransformer_w_JR) == ["visual_dim", "audio_dim", "num_heads",
                                                "hidden_dim", "num_layers", "output_format"]
     assert sig(MultimodalTransformer_wo_JR) == sig(MultimodalTransformer_w_JR)
