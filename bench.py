@@ -468,7 +468,8 @@ def main():
         parity = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv,
                               k=k, H=heads, L=layers)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3" and \
+            jcfg is None:
         cpu = cpu_baseline(model_sd0, fc_sd0, audio, video, lv, la)
 
     if rank == 0:

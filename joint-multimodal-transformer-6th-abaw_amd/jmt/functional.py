@@ -128,11 +128,26 @@ class Rows:
         ok = all(x.stride(a) == x.stride(b) * x.shape[b] for a, b in zip(dims[:-1], dims[1:]))
         ld = x.stride(dims[-1]) if dims else max(x.shape[-1], 1)
         # (a column vector F == 1 with ld == 1 is a dense vector: keep its row order)
-        if not ok or ld < x.shape[-1] or (ld % _vec(x.dtype) and x.shape[-1] > 1) or \
-                x.data_ptr() % 16:
-            x = x.contiguous() if x.data_ptr() % 16 == 0 else x.clone()
-            perm = lead
-            ld = x.shape[-1]
+        F = x.shape[-1]
+        v = _vec(x.dtype)
+        bad_layout = not ok or ld < F
+        if bad_layout or (ld % v and F > 1) or x.data_ptr() % 16:
+            # re-pack: rows in memory order `keep` (the existing order when the layout is
+            # row-regular — other operands of the same GEMMs share it — else the logical one),
+            # row stride padded to the 16-B vector (narrow outputs such as Linear(64, 2))
+            keep = lead if bad_layout else perm
+            Fp = F if (F <= 1 or F % v == 0) else -(-F // v) * v
+            y = torch.empty([x.shape[d] for d in keep] + [Fp], dtype=x.dtype, device=x.device)
+            if Fp != F:
+                y = y[..., :F]
+            inv = [0] * len(keep)
+            for i, d in enumerate(keep):
+                inv[d] = i
+            y = y.permute(*inv, nd - 1)
+            y.copy_(x)
+            x = y
+            perm = keep
+            ld = max(Fp, 1)
             dims = [d for d in perm if x.shape[d] != 1]
         self.t = x
         self.shape = tuple(x.shape)
