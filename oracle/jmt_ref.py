@@ -94,7 +94,10 @@ class emulate_storage:
 # ---------------------------------------------------------------- primitives ------------------
 
 def linear(x, W, b, out_round: bool = True):
-    """nn.Linear: y = x W^T + b (models/fc_layer.py:6-12, two_transformers.py:56)."""
+    """nn.Linear: y = x W^T + b (models/fc_layer.py:6-12, two_transformers.py:56).  fp32: the
+    same fused addmm nn.Linear runs (torch.nn.functional.linear)."""
+    if _EMU["dtype"] is None:
+        return torch.nn.functional.linear(x, W, b)
     y = torch.matmul(rnd(x), rnd(W).t()) + b
     return rnd(y) if out_round else y
 
@@ -106,7 +109,11 @@ def l2_normalize(x, eps: float = 1e-12):
 
 
 def layer_norm(x, g, b, eps: float = 1e-5):
-    """nn.LayerNorm(E) with affine params, biased variance (mm_multi_transformers.py:57-58)."""
+    """nn.LayerNorm(E) with affine params, biased variance (mm_multi_transformers.py:57-58).
+    fp32: torch's layer_norm primitive (what nn.LayerNorm calls); emulated 16-bit storage: the
+    explicit formula with its rounded output."""
+    if _EMU["dtype"] is None:
+        return torch.nn.functional.layer_norm(x, (x.shape[-1],), g, b, eps)
     mu = x.mean(-1, keepdim=True)
     xc = x - mu
     var = (xc * xc).mean(-1, keepdim=True)
@@ -325,18 +332,23 @@ def sgd_nesterov_(params: P, grads: P, bufs: P, lr=1e-4, momentum=0.9, weight_de
                   dampening=0.0):
     """torch.optim.SGD(nesterov=True) as configured by config_file.json:73-80 and
     instantiator.py:32-38.  Params with no grad (final_encoder) are skipped."""
+    keys = [k for k, p in params.items() if grads.get(k) is not None]
+    if not keys:
+        return
     with torch.no_grad():
-        for k, p in params.items():
-            g = grads.get(k)
-            if g is None:
-                continue
-            d = g + weight_decay * p
-            if k not in bufs:
+        ps = [params[k] for k in keys]
+        # d = g + wd p; buf = d (first step) or momentum buf + (1 - dampening) d;
+        # d += momentum buf; p -= lr d  (multi-tensor form of the same per-tensor updates)
+        ds = torch._foreach_add([grads[k] for k in keys], ps, alpha=weight_decay)
+        if keys[0] not in bufs:
+            for k, d in zip(keys, ds):
                 bufs[k] = d.clone()
-            else:
-                bufs[k].mul_(momentum).add_(d, alpha=1 - dampening)
-            d = d + momentum * bufs[k]
-            p.add_(d, alpha=-lr)
+        else:
+            bs = [bufs[k] for k in keys]
+            torch._foreach_mul_(bs, momentum)
+            torch._foreach_add_(bs, ds, alpha=1 - dampening)
+        torch._foreach_add_(ds, [bufs[k] for k in keys], alpha=momentum)
+        torch._foreach_add_(ps, ds, alpha=-lr)
 
 
 def train_step(params: P, fc_params: P, audio_raw, video, labels_v, labels_a, H, L, jm, fmt,
