@@ -188,14 +188,18 @@ def parity_check(model, fc, audio, video, lv, la, cd, jm, fmt, Dv, nwin=2, k=1, 
     from losses.loss import CCCLoss
     crit = CCCLoss(k)
     flat = (lambda o: o.reshape(-1, k)) if k > 1 else (lambda o: o.reshape(1, -1))
+    from jmt import dist as jdist
     a, v = audio[:nwin], video[:nwin]
     T = a.shape[1]
+    group = jdist.loss_group()
+    jdist.set_loss_group(None)       # rank 0 alone: local statistics, no collective
     yv = lv.view(audio.shape[0], T)[:nwin]
     ya = la.view(audio.shape[0], T)[:nwin]
     with torch.no_grad(), JF.compute_mode(cd):
         vo, ao = model(fc(a) if fc is not None else a, v)
         gl1 = float(crit(flat(vo), yv.reshape(1, -1)))
         gl2 = float(crit(flat(ao), ya.reshape(1, -1)))
+    jdist.set_loss_group(group)
     p = {k: t.detach().float().cpu() for k, t in model.state_dict().items()}
     with torch.no_grad():
         ac = a.float().cpu()
@@ -267,6 +271,11 @@ def main():
                     help="eager launches from Python every step")
     ap.add_argument("--probe-steps", type=int, default=3)
     ap.add_argument("--launch-log", default=None, help="write per-launch records (jsonl)")
+    ap.add_argument("--bucket-mb", type=int, default=8,
+                    help="gradient all-reduce bucket size (MiB) for N > 1")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1: all-reduce after the whole backward instead of per bucket "
+                         "as soon as its gradients are complete")
     ap.add_argument("--config-file", default=None,
                     help="a config_file.json (the reference's schema): model_params, the train "
                          "batch / window and the opt__* SGD settings define the workload; further "
@@ -299,7 +308,7 @@ def main():
     from jmt import functional as JF
     from jmt import ops
     from jmt import dist as jdist
-    from jmt.optim import FusedSGD, GradScaler, used_parameters
+    from jmt.optim import FusedSGD, GradScaler
     from jmt.graph import GraphedStep
     from models.two_transformers import Two_transformers
     from models.fc_layer import FcLayer
@@ -363,15 +372,25 @@ def main():
             (scaler.scale(loss) if scaler is not None else loss).backward()
         return loss
 
-    params = used_parameters(fwd_bwd, list(model.parameters()) +
-                             (list(fc.parameters()) if fc is not None else []))
+    # the parameters that get a gradient, laid out in the order their gradients complete, so
+    # that the all-reduce buckets become ready one after another during the backward
+    params, wcounts = jdist.grad_write_profile(fwd_bwd, list(model.parameters()) +
+                                               (list(fc.parameters()) if fc is not None else []))
     opt = FusedSGD(params, **sgd_kw, shadow_dtype=cd if cd != torch.float32 else None)
+    bucketer = None
+    if world > 1 and not args.no_overlap:
+        bucketer = jdist.GradBucketer(opt, wcounts, bucket_bytes=args.bucket_mb << 20,
+                                      group=dist.group.WORLD)
 
     def step():
         opt.zero_grad()
+        if bucketer is not None:
+            bucketer.begin()                     # buckets all-reduce during the backward
         loss = fwd_bwd()
-        if world > 1:
-            bucket = 16 << 20   # elements per all-reduce bucket
+        if bucketer is not None:
+            bucketer.finish()
+        elif world > 1:
+            bucket = 16 << 20   # elements per all-reduce bucket, after the whole backward
             for off in range(0, opt.numel, bucket):
                 dist.all_reduce(opt.flat_g[off:off + bucket])
         if scaler is not None:
@@ -484,6 +503,11 @@ def main():
                        "name": "config_file" if jcfg is not None else args.config,
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
                        "D_a": Da, "D_v": Dv, "parallelism": f"dp{world}",
+                       "grad_allreduce": (None if world == 1 else
+                                          "after backward" if bucketer is None else
+                                          f"{len(bucketer.buckets)} buckets of >= "
+                                          f"{args.bucket_mb} MiB, each as soon as its "
+                                          "gradients are written (overlaps the backward)"),
                        "loss_scaling": "device GradScaler" if scaler is not None else None},
             "roofline": roofline,
             "step_mfma": step_mfma,

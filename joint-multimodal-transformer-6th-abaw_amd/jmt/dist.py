@@ -59,3 +59,137 @@ class FlatGrads:
         for off in range(0, self.numel, self.bucket_elems):
             dist.all_reduce(self.flat[off:off + self.bucket_elems], op=dist.ReduceOp.SUM,
                             group=group)
+
+
+def grad_write_profile(model_fn, params):
+    """Run `model_fn()` (forward + backward) once with gradient-write notifications on: returns
+    the parameters that received a gradient, ordered by when their LAST write was enqueued, and
+    how many writes each gets per backward (the schedule GradBucketer counts down)."""
+    from . import functional as F
+    params = list(params)
+    ids = {id(p): p for p in params}
+    counts, last = {}, {}
+    seq = [0]
+
+    def hook(ps):
+        for p in ps:
+            if id(p) in ids:
+                counts[id(p)] = counts.get(id(p), 0) + 1
+                last[id(p)] = seq[0]
+                seq[0] += 1
+
+    handles = [p.register_post_accumulate_grad_hook(lambda p: hook([p])) for p in params]
+    for p in params:
+        p.grad = None
+    prev, F._grad_hook = F._grad_hook, hook
+    try:
+        model_fn()
+    finally:
+        F._grad_hook = prev
+        for h in handles:
+            h.remove()
+    used = [p for p in params if p.grad is not None]
+    for p in params:
+        p.grad = None
+    missing = [p for p in used if id(p) not in counts]
+    if missing:
+        raise RuntimeError(f"{len(missing)} parameters got a gradient without a write "
+                           "notification (jmt.functional._grad_done)")
+    used.sort(key=lambda p: last[id(p)])
+    return used, {id(p): counts[id(p)] for p in used}
+
+
+class GradBucketer:
+    """The gradient all-reduce overlapped with the backward (the reference's
+    DataParallel reduces after its backward, main.py:487-491): the flat fp32 gradient buffer of
+    FusedSGD — parameters laid out in the order their gradients complete (grad_write_profile) —
+    is cut into contiguous buckets of >= bucket_bytes; each write notification counts its
+    parameter down, and when every parameter of a bucket has had its last write enqueued, an
+    event on the compute stream gates that bucket's SUM all-reduce on a communication stream
+    (RCCL over xGMI with the nccl backend), so it runs under the rest of the backward.
+    finish() issues any bucket still pending and joins the communication into the current
+    stream before the optimizer step."""
+
+    def __init__(self, opt, counts, bucket_bytes: int = 16 << 20, group=None):
+        from . import functional as F
+        self._F = F
+        self.flat = opt.flat_g
+        self.group = group
+        self.expected = {}
+        self.bucket_of = {}
+        self.buckets = []          # (lo, hi, n_params)
+        lo, cur, nbytes = 0, [], 0
+        ends = [off + -(-p.numel() // 64) * 64 for p, off in zip(opt.params, opt.offsets)]
+        for i, p in enumerate(opt.params):
+            if id(p) not in counts:
+                raise RuntimeError("GradBucketer: a parameter of the optimizer has no write "
+                                   "profile")
+            self.expected[id(p)] = counts[id(p)]
+            cur.append(p)
+            nbytes += p.numel() * 4
+            if nbytes >= bucket_bytes or i == len(opt.params) - 1:
+                for q in cur:
+                    self.bucket_of[id(q)] = len(self.buckets)
+                self.buckets.append((lo, ends[i], len(cur)))
+                lo, cur, nbytes = ends[i], [], 0
+        self.cuda = self.flat.is_cuda
+        self.comm = torch.cuda.Stream(self.flat.device) if self.cuda else None
+        self._hooks = [p.register_post_accumulate_grad_hook(lambda p: F._grad_done(p))
+                       for p in opt.params]
+        self.launch_log = []
+
+    def begin(self):
+        self.left = dict(self.expected)
+        self.bucket_left = [b[2] for b in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        self.works = []
+        self.launch_log = []
+        self._F._grad_hook = self._done
+
+    def _done(self, ps):
+        for p in ps:
+            k = id(p)
+            if k not in self.left:
+                continue
+            self.left[k] -= 1
+            if self.left[k] == 0:
+                b = self.bucket_of[k]
+                self.bucket_left[b] -= 1
+                if self.bucket_left[b] == 0:
+                    self._launch(b)
+
+    def _launch(self, b):
+        import torch.distributed as dist
+        if self.launched[b]:
+            return
+        self.launched[b] = True
+        self.launch_log.append(b)
+        lo, hi, _ = self.buckets[b]
+        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record()                                   # after the bucket's last write
+            self.comm.wait_event(ev)
+            with torch.cuda.stream(self.comm):
+                self.works.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM,
+                                                  group=self.group, async_op=True))
+        else:
+            self.works.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM,
+                                              group=self.group, async_op=True))
+
+    def finish(self):
+        self._F._grad_hook = None
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
+        for w in self.works:
+            w.wait()
+        if self.cuda:
+            torch.cuda.current_stream().wait_stream(self.comm)
+        self.works = []
+
+    def close(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

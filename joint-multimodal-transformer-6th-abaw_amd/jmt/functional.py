@@ -100,6 +100,16 @@ def register_shadow(w: torch.Tensor, shadow: Optional[torch.Tensor]):
     w._jmt_shadow = None
 
 
+# Set by jmt.dist.GradBucketer: called with the parameters whose gradient writes have just been
+# enqueued on the current stream (the last write of a parameter makes its bucket ready).
+_grad_hook = None
+
+
+def _grad_done(*ps) -> None:
+    if _grad_hook is not None:
+        _grad_hook([p for p in ps if p is not None and p.requires_grad])
+
+
 def _grad_buffer(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     if p is None or not p.requires_grad:
         return None
@@ -253,12 +263,14 @@ def _wgrad(G: Rows, n, xin, ld_in, kseg, W, r0, cd):
              b_mode=1 if nseg > 1 else 0,
              c=[_ptr(gW, r0 * Kin)], ldc=Kin, batch0=nseg, sA=(0, 0), sB=(0, 0),
              sC=(kseg, 0), beta=1.0, device=G.t.device)
+    _grad_done(W)
 
 
 def _bgrad(G: Rows, n, b, r0):
     gb = _grad_buffer(b)
     if gb is not None:
         ops.colsum(G.t, G.ld, G.rows, n, gb[r0:r0 + n], beta_acc=True)
+        _grad_done(b)
 
 
 # ------------------------------------------------------------------------- Linear
@@ -445,6 +457,7 @@ class AddLayerNormFn(Function):
         ops.layernorm_bwd(x, L.ld, r, ldr, G.t, G.ld, mean, rstd, gamma, dx, _ld(dx, L.perm),
                           dg if dg is not None else tmp[0], db if db is not None else tmp[1],
                           True if tmp is None else False, L.rows, L.F)
+        _grad_done(gamma, beta)
         dxx = dx if xdt == cd else _cast_keep_layout(dx, xdt)
         drr = None
         if r is not None:

@@ -29,8 +29,8 @@ import torch
 from torch.autograd import Function
 
 from . import ops
-from .functional import (_dc, _grad_buffer, _ptr, attn_backward, attn_forward, compute_dtype,
-                         weight_as)
+from .functional import (_dc, _grad_buffer, _grad_done, _ptr, attn_backward, attn_forward,
+                         compute_dtype, weight_as)
 
 _enabled = {"on": os.environ.get("JMT_GROUPED", "1") != "0"}
 
@@ -97,12 +97,14 @@ def _gemm_wgrad(dy_ptrs: Sequence[int], ldy: int, sdy: int, x_ptrs: Sequence[int
              sB=(0 if tb else sx, 0),
              c=[_ptr(g, r0 * Kin) for g in grads], ldc=Kin, c_mode=1, batch0=len(Ws),
              beta=1.0, device=dev)
+    _grad_done(*Ws)
 
 
 def _bias_grad(dy2: torch.Tensor, ld: int, rows: int, n: int, b, r0: int):
     gb = _grad_buffer(b)
     if gb is not None:
         ops.colsum(dy2, ld, rows, n, gb[r0:r0 + n], beta_acc=True)
+        _grad_done(b)
 
 
 def _bias_grad_grouped(dy_ptr: int, G: int, ld: int, sdy: int, rows: int, n: int, bs, r0: int,
@@ -115,6 +117,7 @@ def _bias_grad_grouped(dy_ptr: int, G: int, ld: int, sdy: int, rows: int, n: int
         dbs.append(gb[r0:r0 + n] if gb is not None else
                    torch.empty(n, dtype=torch.float32, device=dev))
     ops.colsum_grouped(dy_ptr, _dc(cd), G, ld, sdy, rows, n, dbs, beta_acc=True, device=dev)
+    _grad_done(*bs)
 
 
 def _contig(t: torch.Tensor, cd) -> torch.Tensor:
@@ -230,6 +233,7 @@ class EncoderGroupFn(Function):
                 ops.layernorm_bwd(x[g], E, r[g], E, dy[g], E, st[0, g * R:], st[1, g * R:],
                                   gamma[g], dx[g], E, dgam if dgam is not None else tmp[0],
                                   dbet if dbet is not None else tmp[1], tmp is None, R, E)
+                _grad_done(gamma[g], beta[g])
 
         # LN2: dS2 = d(H1 + F2)
         dS = torch.empty(G, B, T, E, dtype=cd, device=dev)
@@ -455,6 +459,7 @@ class ConcatLinearFn(Function):
                      a=[dy.data_ptr()], lda=N, a_kmajor=False, sA=(0, 0),
                      b=[X.data_ptr()], ldb=E, b_kmajor=False, sB=(R * E, 0),
                      c=[gW.data_ptr()], ldc=S * E, sC=(E, 0), batch0=S, beta=1.0, device=dev)
+            _grad_done(W)
         if b is not None:
             _bias_grad(dy, N, R, N, b, 0)
         return dX, None, None

@@ -39,6 +39,7 @@ class FusedSGD:
         self.shadow = (torch.empty(n, dtype=shadow_dtype, device=dev)
                        if shadow_dtype not in (None, torch.float32) else None)
         self.flat_p.zero_()
+        self.offsets = offs
         self._gviews = []
         with torch.no_grad():
             for p, off in zip(self.params, offs):

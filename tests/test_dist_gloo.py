@@ -5,6 +5,8 @@ flat gradient buffer (jmt.dist.FlatGrads) — checked against the reference's Da
 semantics: replicas on dim-0 shards, outputs gathered on dim 0, loss on the gathered batch
 (main.py:487-491, train.py:303-311)."""
 import os
+
+import numpy as np
 import socket
 
 import pytest
@@ -139,3 +141,75 @@ def test_shard_pairing_equals_dataparallel_gather():
         pairs_rank |= set(zip(preds[:, lo:hi].reshape(-1).tolist(),
                               labels[lo:hi].reshape(-1).tolist()))
     assert pairs_dp == pairs_rank
+
+
+class _FakeOpt:
+    """The slice of FusedSGD that GradBucketer reads: params, their flat offsets, flat_g."""
+
+    def __init__(self, sizes):
+        self.params = [torch.nn.Parameter(torch.zeros(n)) for n in sizes]
+        self.offsets, n = [], 0
+        for p in self.params:
+            self.offsets.append(n)
+            n += -(-p.numel() // 64) * 64
+        self.flat_g = torch.zeros(n)
+
+
+def _bucket_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from jmt import dist as jdist
+        from jmt import functional as JF
+        sizes = [300, 70, 1000, 5, 64, 2000]
+        opt = _FakeOpt(sizes)
+        counts = {id(p): c for p, c in zip(opt.params, [1, 2, 1, 3, 1, 1])}
+        b = jdist.GradBucketer(opt, counts, bucket_bytes=1200 * 4)
+        logs = []
+        for step in range(2):
+            opt.flat_g.zero_()
+            b.begin()
+            # a backward's writes, in the layout order, some parameters written several times
+            for i, p in enumerate(opt.params):
+                off = opt.offsets[i]
+                for w in range(counts[id(p)]):
+                    opt.flat_g[off:off + p.numel()] += (rank + 1) * (i + 1) * (w + 1)
+                    JF._grad_done(p)
+                logs.append((step, i, list(b.launch_log)))
+            b.finish()
+            q.put((rank, step, opt.flat_g.clone().numpy(), b.buckets, logs))
+        b.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_bucketer_launches_each_bucket_when_complete_and_sums():
+    """jmt.dist.GradBucketer on two gloo ranks: buckets are contiguous and >= the byte size, a
+    bucket is issued exactly when the last write of its last parameter is notified (never
+    before: that would reduce a half-written gradient), and after finish() every rank holds
+    the SUM over ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    out = [q.get(timeout=300) for _ in range(4)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    sizes = [300, 70, 1000, 5, 64, 2000]
+    counts = [1, 2, 1, 3, 1, 1]
+    for rank, step, flat, buckets, logs in out:
+        # params 0-2 (1370 floats) close bucket 0, 3-5 the last one
+        assert [(b[2]) for b in buckets] == [3, 3]
+        assert buckets[0][0] == 0 and buckets[0][1] == buckets[1][0]
+        for st, i, launched in logs:
+            if st != step:
+                continue
+            assert launched == ([] if i < 2 else [0] if i < 5 else [0, 1]), (i, launched)
+        off = 0
+        for i, n in enumerate(sizes):
+            want = sum((r + 1) * (i + 1) * (w + 1) for r in range(2) for w in range(counts[i]))
+            assert np.all(flat[off:off + n] == want), (i, flat[off], want)
+            off += -(-n // 64) * 64

@@ -232,3 +232,75 @@ def test_two_rank_losses_unequal_shards_match_gathered_batch(kind):
         gr = x.grad[off:off + SIZES[rank]].numpy()
         assert np.abs(g - gr).max() <= 1e-5 * max(1.0, np.abs(gr).max()), (rank, g, gr)
         off += SIZES[rank]
+
+
+def _bucketed_worker(rank, world, port, q):
+    """bench.py's N>1 step: FusedSGD's flat gradients in write-completion order and the
+    all-reduce issued bucket by bucket during the backward (jmt.dist.GradBucketer)."""
+    dist, jdist = _init(rank, world, port)
+    try:
+        from jmt import functional as JF
+        from jmt.optim import FusedSGD
+        from losses.loss import CCCLoss
+        audio, video, lv, la = _inputs()
+        lo, hi = jdist.shard_range(B, rank, world)
+        m = _model().cuda()
+        crit = CCCLoss(1)
+        a, v = audio[lo:hi].cuda(), video[lo:hi].cuda()
+        n = (hi - lo) * T
+        yv, ya = lv[lo:hi].cuda().view(-1, n), la[lo:hi].cuda().view(-1, n)
+
+        def fwd_bwd():
+            with JF.compute_mode(torch.float32):
+                vo, ao = m(a, v)
+                loss = crit(vo.view(-1, n), yv) + crit(ao.view(-1, n), ya)
+                loss.backward()
+            return loss
+
+        params, counts = jdist.grad_write_profile(fwd_bwd, list(m.parameters()))
+        opt = FusedSGD(params, lr=0.0)
+        bk = jdist.GradBucketer(opt, counts, bucket_bytes=1 << 20, group=dist.group.WORLD)
+        opt.zero_grad()
+        bk.begin()
+        loss = fwd_bwd()
+        early = len(bk.launch_log)             # buckets issued before the backward returned
+        bk.finish()
+        torch.cuda.synchronize()
+        names = {id(p): k for k, p in m.named_parameters()}
+        grads = {names[id(p)]: p.grad.detach().cpu().numpy() for p in params}
+        q.put((rank, float(loss.detach()), grads, early, len(bk.buckets)))
+        bk.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_overlapped_bucket_allreduce_matches_dataparallel_oracle():
+    out = sorted(_spawn_raw(_bucketed_worker), key=lambda r: r[0])
+    ref_loss, ref_grads = _dp_oracle()
+    gmax = max(float(g.abs().max()) for g in ref_grads.values())
+    (_, l0, g0, early0, nb), (_, l1, g1, _, _) = out
+    assert nb > 2 and early0 >= 1, (nb, early0)   # several buckets, some issued mid-backward
+    assert abs(l0 - ref_loss) <= 1e-5, (l0, ref_loss)
+    assert set(g0) == set(ref_grads), set(g0) ^ set(ref_grads)
+    for k in g0:
+        assert np.array_equal(g0[k], g1[k]), k
+        r = ref_grads[k]
+        err = float((torch.from_numpy(g0[k]) - r).abs().max())
+        assert err <= 1e-4 * max(float(r.abs().max()), 0.01 * gmax), (k, err)
+
+
+def _spawn_raw(target, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = [q.get(timeout=240) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for p in procs:
+        assert p.exitcode == 0, p.exitcode
+    return out
