@@ -100,6 +100,11 @@ using Cfg11 = TileCfg<128, 128, 2, 2, 64, 3, 1, 1, 0, 3>;
 using Cfg20 = TileCfg<256, 256, 2, 4, 64, 4, 1, 1, 0, 0, 1>;
 // 128x128, 64-B K-tiles, 4 stages, interleaved issue, 2 blocks / CU
 using Cfg21 = TileCfg<128, 128, 2, 2, 64, 4, 1, 1, 0, 2, 1>;
+// (256x256 over 4 waves — 2x2, 128x128 each, 256 accumulators per lane in AGPRs, 64-B K-tiles,
+// 4 stages, one block / CU: the macro tile hipBLASLt picks on these shapes, profiles/
+// r02_hipblaslt_reference.txt — compiled without spills but measured 1.45-1.65x slower than
+// Cfg5 / Cfg20 on every step shape, with and without interleaved DMA issue: one wave per SIMD
+// leaves each wave's LDS-read latency exposed; profiles/r02_gemm_4wave_256.txt)
 // (without s_setprio the two measured the same: profiles/r01_gemm_occupancy.txt)
 // (8-wave 128x256 / 256x128 tiles with 64-B K-tiles, 3 stages, 2 blocks / CU measured 20-100%
 // slower on every step shape: profiles/r01_gemm_occupancy.txt)
@@ -998,7 +1003,11 @@ static void plan(int dt, int M, int N, int K, int batch, int fixed_splits, int& 
   splits = fixed_splits > 0 ? fixed_splits : 1;
   for (int i = 0; i < nm; ++i) {
     if (!tile_ok(ms[i], M, N)) continue;
-    int s_lo = 1, s_hi = 32;
+    // a handful of output tiles over a long K (the V / A regressors' 1 x 128 weight gradient over
+    // all B*T rows): up to 256 splits, so the launch still covers the chip
+    const long tiles = (long)((M + ms[i].bm - 1) / ms[i].bm) * ((N + ms[i].bn - 1) / ms[i].bn) *
+                       batch;
+    int s_lo = 1, s_hi = tiles <= 8 ? 256 : 32;
     if (fixed_splits > 0) s_lo = s_hi = fixed_splits;
     for (int s = s_lo; s <= s_hi; ++s) {
       if (fixed_splits <= 0 && s > 1 && K / s < 4 * bke) break;   // >= 4 K-tiles per split

@@ -172,8 +172,13 @@ __global__ __launch_bounds__(64 * SA_WPB) void small_attn_bwd_kernel(SmallAttnAr
   }
 }
 
+template <typename T, int LK, bool BWD>
+static bool launch_static(int Lq, const SmallAttnArgs& a, hipStream_t st);
+
 template <int LK, bool BWD>
 static void launch_lk(int dt, const SmallAttnArgs& a, hipStream_t st) {
+  if (dt == JMT_BF16 && launch_static<__bf16, LK, BWD>(a.Lq, a, st)) return;
+  if (dt == JMT_F16 && launch_static<_Float16, LK, BWD>(a.Lq, a, st)) return;
   const dim3 grid((unsigned)((a.N + SA_WPB - 1) / SA_WPB)), block(64 * SA_WPB);
 #define JMT_SA(T)                                                                           \
   if (BWD) hipLaunchKernelGGL((small_attn_bwd_kernel<T, LK>), grid, block, 0, st, a);       \
@@ -182,6 +187,171 @@ static void launch_lk(int dt, const SmallAttnArgs& a, hipStream_t st) {
   else if (dt == JMT_BF16) { JMT_SA(__bf16) }
   else { JMT_SA(_Float16) }
 #undef JMT_SA
+}
+
+// ---- 16-bit, Lq fixed at compile time (Lq == Lk: self-attention; Lq == 1: last-token query):
+// every row load and P read of a sequence is issued before the first use, so a wave pays ONE
+// memory latency per sequence instead of one per query row (the runtime-Lq kernels above walk
+// the query rows in a loop whose loads wait on each other's iteration).  Rows stay packed
+// (one 16-B register quad each) until used.
+template <typename T>
+__device__ __forceinline__ void unpack8(const uint4& u, float (&x)[8]) {
+  const T* h = (const T*)&u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = (float)h[e];
+}
+
+template <typename T, int LK, int LQ>
+__global__ __launch_bounds__(64 * SA_WPB) void small_attn_fwd_static(SmallAttnArgs p) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * SA_WPB + (threadIdx.x >> 6);
+  if (n >= p.N) return;
+  const int G = SA_E / 8 / p.H;
+  const int hd = lane / G;
+  const int c = 8 * lane;
+  uint4 kr[LK], vr[LK], qr[LQ];
+#pragma unroll
+  for (int j = 0; j < LK; ++j) {
+    kr[j] = *(const uint4*)((const T*)p.k + (int64_t)n * p.sk_n + (int64_t)j * p.sk_l + c);
+    vr[j] = *(const uint4*)((const T*)p.v + (int64_t)n * p.sv_n + (int64_t)j * p.sv_l + c);
+  }
+#pragma unroll
+  for (int i = 0; i < LQ; ++i)
+    qr[i] = *(const uint4*)((const T*)p.q + (int64_t)n * p.sq_n + (int64_t)i * p.sq_l + c);
+#pragma unroll
+  for (int i = 0; i < LQ; ++i) {
+    float q[8];
+    unpack8<T>(qr[i], q);
+    float s[LK], mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < LK; ++j) {
+      float kk[8];
+      unpack8<T>(kr[j], kk);
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf(q[e], kk[e], d);
+      s[j] = group_sum(d, G) * p.scale;
+      mx = fmaxf(mx, s[j]);
+    }
+    float l = 0.f;
+#pragma unroll
+    for (int j = 0; j < LK; ++j) {
+      s[j] = __expf(s[j] - mx);
+      l += s[j];
+    }
+    const float inv = 1.f / l;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < LK; ++j) {
+      s[j] *= inv;
+      float vv[8];
+      unpack8<T>(vr[j], vv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(s[j], vv[e], o[e]);
+    }
+    store8((T*)p.o + (int64_t)n * p.so_n + (int64_t)i * p.so_l + c, o);
+    if (p.p && (lane % G) == 0) {
+      float* pr = p.p + (((int64_t)n * p.H + hd) * LQ + i) * LK;
+#pragma unroll
+      for (int j = 0; j < LK; ++j) pr[j] = s[j];
+    }
+  }
+}
+
+template <typename T, int LK, int LQ>
+__global__ __launch_bounds__(64 * SA_WPB) void small_attn_bwd_static(SmallAttnArgs p) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * SA_WPB + (threadIdx.x >> 6);
+  if (n >= p.N) return;
+  const int G = SA_E / 8 / p.H;
+  const int hd = lane / G;
+  const int c = 8 * lane;
+  uint4 kr[LK], vr[LK], qr[LQ], gr[LQ];
+  float P[LQ][LK];
+#pragma unroll
+  for (int j = 0; j < LK; ++j) {
+    kr[j] = *(const uint4*)((const T*)p.k + (int64_t)n * p.sk_n + (int64_t)j * p.sk_l + c);
+    vr[j] = *(const uint4*)((const T*)p.v + (int64_t)n * p.sv_n + (int64_t)j * p.sv_l + c);
+  }
+  const float* pb = p.p + ((int64_t)n * p.H + hd) * LQ * LK;
+#pragma unroll
+  for (int i = 0; i < LQ; ++i) {
+    qr[i] = *(const uint4*)((const T*)p.q + (int64_t)n * p.sq_n + (int64_t)i * p.sq_l + c);
+    gr[i] = *(const uint4*)((const T*)p.go + (int64_t)n * p.so_n + (int64_t)i * p.so_l + c);
+#pragma unroll
+    for (int j = 0; j < LK; ++j) P[i][j] = pb[i * LK + j];
+  }
+  // dS = scale P o (dP - rowsum(P o dP)),  dP_ij = dO_i . V_j
+  float dS[LQ][LK];
+#pragma unroll
+  for (int i = 0; i < LQ; ++i) {
+    float g[8];
+    unpack8<T>(gr[i], g);
+    float dsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < LK; ++j) {
+      float vv[8];
+      unpack8<T>(vr[j], vv);
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf(g[e], vv[e], d);
+      dS[i][j] = group_sum(d, G);
+      dsum = fmaf(P[i][j], dS[i][j], dsum);
+    }
+#pragma unroll
+    for (int j = 0; j < LK; ++j) dS[i][j] = p.scale * P[i][j] * (dS[i][j] - dsum);
+  }
+#pragma unroll
+  for (int i = 0; i < LQ; ++i) {                               // dQ_i = sum_j dS_ij K_j
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < LK; ++j) {
+      float kk[8];
+      unpack8<T>(kr[j], kk);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf(dS[i][j], kk[e], acc[e]);
+    }
+    store8((T*)p.dq + (int64_t)n * p.sdq_n + (int64_t)i * p.sdq_l + c, acc);
+  }
+#pragma unroll
+  for (int j = 0; j < LK; ++j) {                               // dK_j, dV_j
+    float ak[8], av[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { ak[e] = 0.f; av[e] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < LQ; ++i) {
+      float qq[8], gg[8];
+      unpack8<T>(qr[i], qq);
+      unpack8<T>(gr[i], gg);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ak[e] = fmaf(dS[i][j], qq[e], ak[e]);
+        av[e] = fmaf(P[i][j], gg[e], av[e]);
+      }
+    }
+    store8((T*)p.dk + (int64_t)n * p.sdk_n + (int64_t)j * p.sdk_l + c, ak);
+    store8((T*)p.dv + (int64_t)n * p.sdv_n + (int64_t)j * p.sdv_l + c, av);
+  }
+}
+
+template <typename T, int LK, bool BWD>
+static bool launch_static(int Lq, const SmallAttnArgs& a, hipStream_t st) {
+  const dim3 grid((unsigned)((a.N + SA_WPB - 1) / SA_WPB)), block(64 * SA_WPB);
+  if (Lq == LK) {
+    if (BWD) hipLaunchKernelGGL((small_attn_bwd_static<T, LK, LK>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((small_attn_fwd_static<T, LK, LK>), grid, block, 0, st, a);
+    return true;
+  }
+  if (Lq == 1) {
+    if (BWD) hipLaunchKernelGGL((small_attn_bwd_static<T, LK, 1>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((small_attn_fwd_static<T, LK, 1>), grid, block, 0, st, a);
+    return true;
+  }
+  return false;
 }
 
 template <bool BWD>

@@ -232,8 +232,9 @@ def _linear_fwd(xin, ld_in, rows, kseg, W, r0, n, b, y, ldy, cd, relu=False):
              device=y.device)
 
 
-def _dgrad(G: Rows, n, W, r0, cd, outs, ld_out, nseg, kseg, aux=None, ldaux=0):
-    """outs[s] = (dY . W[r0:r0+n, s*kseg:(s+1)*kseg]) (masked by aux > 0)."""
+def _dgrad(G: Rows, n, W, r0, cd, outs, ld_out, nseg, kseg, aux=None, ldaux=0, beta=0.0):
+    """outs[s] = (dY . W[r0:r0+n, s*kseg:(s+1)*kseg]) (masked by aux > 0; beta = 1 adds to the
+    existing outs)."""
     Wc = weight_as(W, cd)
     Kin = Wc.shape[1]
     if n == 1:   # dY is a column: read it as an MN-major operand (row stride irrelevant)
@@ -244,7 +245,7 @@ def _dgrad(G: Rows, n, W, r0, cd, outs, ld_out, nseg, kseg, aux=None, ldaux=0):
              a=[G.t.data_ptr()], lda=a_ld, a_kmajor=a_kmaj,
              b=[_ptr(Wc, r0 * Kin)], ldb=Kin, b_kmajor=False,
              c=[o.data_ptr() for o in outs], ldc=ld_out, c_mode=1 if nseg > 1 else 0,
-             batch0=nseg, sA=(0, 0), sB=(kseg, 0), sC=(0, 0),
+             batch0=nseg, sA=(0, 0), sB=(kseg, 0), sC=(0, 0), beta=beta,
              aux=aux, ldaux=ldaux, device=G.t.device)
 
 

@@ -154,6 +154,53 @@ def stack_groups(*xs) -> torch.Tensor:
     return StackGroupsFn.apply(*xs)
 
 
+class StackJointFn(Function):
+    """X = stack(v, p, cat(v, p) W^T + b) -> (3, B, T, E): the two streams and the joint
+    representation of out_layer_pv (mm_multi_transformers.py:120-124) in one stacked buffer;
+    the K-concatenated GEMM writes the third slot directly.  The backward adds out_layer_pv's
+    input gradients into the first two slots of the incoming dX with the dgrad GEMM's beta = 1
+    epilogue, so the two uses of v and p need no separate gradient sum."""
+
+    @staticmethod
+    def forward(ctx, v, p, W, b):
+        from .functional import _linear_fwd
+        cd = compute_dtype()
+        B, T, E = v.shape
+        assert tuple(p.shape) == (B, T, E) and W.shape == (E, 2 * E), (v.shape, p.shape, W.shape)
+        X = torch.empty(3, B, T, E, dtype=cd, device=v.device)
+        for g, x in enumerate((v, p)):
+            if x.stride(-1) != 1 or x.stride(1) != E * x.stride(2) or \
+                    x.stride(0) != T * x.stride(1):
+                x = x.contiguous()
+            ops.copy2d(x.data_ptr(), ops.dt(x), X[g].data_ptr(), ops.dt(X), B * T, E,
+                       x.stride(1), 1, E, 1)
+        _linear_fwd([X[0], X[1]], E, B * T, E, W, 0, E, b, X[2], E, cd)
+        ctx.save_for_backward(X, W, b)
+        ctx.meta = (cd, v.dtype, p.dtype)
+        return X
+
+    @staticmethod
+    def backward(ctx, dX):
+        from .functional import Rows, _bgrad, _cast_keep_layout, _dgrad, _wgrad
+        X, W, b = ctx.saved_tensors
+        cd, vdt, pdt = ctx.meta
+        G3, B, T, E = X.shape
+        # the incoming gradient is this Function's alone (the stacked X feeds the encoder group
+        # only): its first two slots receive out_layer_pv's input gradients in place
+        dX = _contig(dX, cd)
+        G = Rows(dX[2])
+        _dgrad(G, E, W, 0, cd, [dX[0], dX[1]], E, 2, E, beta=1.0)
+        _wgrad(G, E, [X[0], X[1]], E, E, W, 0, cd)
+        _bgrad(G, E, b, 0)
+        dv = dX[0] if vdt == cd else _cast_keep_layout(dX[0], vdt)
+        dp = dX[1] if pdt == cd else _cast_keep_layout(dX[1], pdt)
+        return dv, dp, None, None
+
+
+def stack_joint(v, p, W, b) -> torch.Tensor:
+    return StackJointFn.apply(v, p, W, b)
+
+
 # ------------------------------------------------------------------------- encoder group
 def encoder_layer_params(layer) -> List[torch.Tensor]:
     """The 12 parameters of one TransformerEncoderLayer (mm_multi_transformers.py:48-70)."""

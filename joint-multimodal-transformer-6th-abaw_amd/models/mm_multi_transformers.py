@@ -115,12 +115,11 @@ class MultimodalTransformer_w_JR(nn.Module):
             raise NotImplementedError(output_format)
 
     def forward(self, visual_features, physiological_features):
+        if grouped.enabled() and visual_features.shape == physiological_features.shape:
+            return self._forward_grouped(visual_features, physiological_features)
         # cat + out_layer_pv as ONE K-concatenated GEMM (:120-124)
         joint_representation = F.linear((visual_features, physiological_features),
                                         self.out_layer_pv.weight, self.out_layer_pv.bias)
-        if grouped.enabled() and visual_features.shape == physiological_features.shape:
-            return self._forward_grouped(visual_features, physiological_features,
-                                         joint_representation)
         v = visual_features.permute(1, 0, 2)          # free: a strided view (:127-129)
         p = physiological_features.permute(1, 0, 2)
         j = joint_representation.permute(1, 0, 2)
@@ -157,11 +156,13 @@ class MultimodalTransformer_w_JR(nn.Module):
         # FC head (:201-211): torch.cat of the 6 outputs never materialised (K-concat GEMM)
         return F.linear(tuple(outs), self.out_layer1.weight, self.out_layer1.bias)
 
-    def _forward_grouped(self, visual_features, physiological_features, joint_representation):
+    def _forward_grouped(self, visual_features, physiological_features):
         """Same math, batched across the parallel branches (jmt/grouped.py): the three streams
-        in one stacked (3, B, T, E) buffer, each encoder layer of the three encoders as one
-        grouped launch sequence, the six cross-attentions as one (:132-167)."""
-        X = grouped.stack_groups(visual_features, physiological_features, joint_representation)
+        in one stacked (3, B, T, E) buffer — out_layer_pv's K-concatenated GEMM (:120-124)
+        writing the joint representation into its third slot — each encoder layer of the three
+        encoders as one grouped launch sequence, the six cross-attentions as one (:132-167)."""
+        X = grouped.stack_joint(visual_features, physiological_features,
+                                self.out_layer_pv.weight, self.out_layer_pv.bias)
         for lv, lp, lj in zip(self.visual_encoder.layers, self.physiological_encoder.layers,
                               self.joint_representation_encoder.layers):
             X = grouped.encoder_group(X, [lv, lp, lj], self.num_heads)
