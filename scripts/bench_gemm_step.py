@@ -39,7 +39,7 @@ def make_shapes(R):
 SHAPES = make_shapes(R)
 
 
-def run(reps, cfg, dbg=0):
+def run(reps, cfg, dbg=0, splits=None):
     lib = _lib.load()
     lib.jmt_gemm_set_debug(dbg | (cfg << 8))
     dev = "cuda"
@@ -57,7 +57,8 @@ def run(reps, cfg, dbg=0):
         aux = torch.randn(batch, M * N, device=dev).bfloat16() if ex.get("aux") else None
         kw = dict(M=M, N=N, K=K, ab_dtype=BF16, c_dtype=cdt, lda=lda, a_kmajor=ak, ldb=ldb,
                   b_kmajor=bk, c=[c.data_ptr()], ldc=N, batch0=batch, sC=(M * N, 0),
-                  beta=ex.get("beta", 0.0), aux=aux, ldaux=N if aux is not None else 0, device=dev)
+                  beta=ex.get("beta", 0.0), aux=aux, ldaux=N if aux is not None else 0, device=dev,
+                  splits=splits)
         if kc:
             kw.update(a=[a.data_ptr() for a in A], a_mode=2, a_kseg=K // kc,
                       b=[b.data_ptr() for b in Bt], b_mode=2, b_kseg=K // kc)
@@ -79,8 +80,8 @@ def run(reps, cfg, dbg=0):
         us = s.elapsed_time(e) / reps * 1e3
         fl = 2.0 * M * N * K * batch
         by = (M * K + N * K) * 2 * batch + M * N * c.element_size() * batch
-        splits = ops.auto_splits(M, N, K, batch, BF16)
-        print(json.dumps({"shape": name, "cfg": cfg, "dbg": dbg, "splits": splits, "us": round(us, 2),
+        splits_used = splits or ops.auto_splits(M, N, K, batch, BF16)
+        print(json.dumps({"shape": name, "cfg": cfg, "dbg": dbg, "splits": splits_used, "us": round(us, 2),
                           "tflops": round(fl / us / 1e6, 1), "gbs": round(by / us / 1e3, 1)}),
               flush=True)
         del ws
@@ -94,10 +95,12 @@ if __name__ == "__main__":
     ap.add_argument("--only", default="")
     ap.add_argument("--dbg", type=int, nargs="*", default=[0])
     ap.add_argument("--rows", type=int, default=R, help="tokens per stream (realdata: 1024)")
+    ap.add_argument("--splits", type=int, nargs="*", default=[0], help="forced split-K (0: planner)")
     args = ap.parse_args()
     SHAPES[:] = make_shapes(args.rows)
     if args.only:
         SHAPES[:] = [s for s in SHAPES if args.only in s[0]]
     for c in args.cfg:
         for d in args.dbg:
-            run(args.reps, c, d)
+            for sp in args.splits:
+                run(args.reps, c, d, sp or None)

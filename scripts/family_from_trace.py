@@ -1,0 +1,93 @@
+"""Per-family kernel time from a rocprofv3 --kernel-trace database, in bench.py's families
+(GEMM by operand majorness NT / NN / TN / TT, attention fwd / bwd, small attention fwd / bwd),
+next to the in-step figures bench.py printed in the same command:
+
+    python scripts/family_from_trace.py gpurun_out/prof/run_results.db gpurun_out/bench.log \
+        [--steps 200]
+
+A GEMM launch with split-K is two kernels (the tile kernel and splitk_reduce_kernel); bench.py's
+event pair brackets both, so the reduce kernels are attributed to the family of the GEMM
+dispatched right before them.  Trace time per step = family kernel time in the timed region
+(the last `--steps` graph replays: the kernels between the first and last dispatch of the timed
+steps are selected by count) ÷ steps."""
+import argparse
+import json
+import re
+import sqlite3
+from collections import defaultdict
+
+MANGLED = re.compile(r"gemm_kernel.*?Lb([01])ELb([01])E")
+DEMANGLED = re.compile(r"gemm_kernel<.*?(true|false), (true|false), jmt::TileCfg")
+
+
+def family(name: str):
+    if "gemm_kernel" in name:
+        m = MANGLED.search(name)
+        if m:
+            ak, bk = m.group(1) == "1", m.group(2) == "1"
+        else:
+            m = DEMANGLED.search(name)
+            if not m:
+                return "gemm_?"
+            ak, bk = m.group(1) == "true", m.group(2) == "true"
+        return {(True, True): "gemm_NT", (True, False): "gemm_NN", (False, False): "gemm_TN",
+                (False, True): "gemm_TT"}[(ak, bk)]
+    if "splitk_reduce" in name:
+        return "reduce"
+    if "small_attn_fwd" in name:
+        return "small_attn_fwd"
+    if "small_attn_bwd" in name:
+        return "small_attn_bwd"
+    if "attn_fwd_kernel" in name:
+        return "attn_fwd"
+    if "attn_bwd_kernel" in name:
+        return "attn_bwd"
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("bench_log")
+    args = ap.parse_args()
+    line = [l for l in open(args.bench_log) if l.startswith("{")][-1]
+    bench = json.loads(line)
+    steps = bench["steps"]
+    fams = {f["family"]: f for f in bench["roofline"]["families"]}
+    c = sqlite3.connect(args.db)
+    rows = c.execute("select name, start, end, duration from kernels order by start").fetchall()
+    # the timed region: bench.py's probe steps come after it and launch jmt_noop / the torch
+    # sleep kernel around every hooked launch; the graph replays before them carry none
+    first_probe = next((i for i, r in enumerate(rows) if "noop_kernel" in r[0]), len(rows))
+    per_step_n = None
+    timed = rows[:first_probe]
+    # dispatches per step = those of one replay: count launches of the CCC finish kernel
+    finish = [i for i, r in enumerate(timed) if "ccc_finish_kernel" in r[0]]
+    per_loss = 2
+    if len(finish) >= per_loss * (steps + 1):
+        lo = finish[-per_loss * steps - 1] + 1
+        timed = timed[lo:]
+        per_step_n = len(timed) / steps
+    agg = defaultdict(float)
+    last = None
+    for name, s, e, d in timed:
+        f = family(name)
+        if f == "reduce":
+            f = last
+        if f is not None:
+            agg[f] += d
+            if not f.startswith("reduce"):
+                last = f
+    print(f"bench: {bench['metric']}  {bench['value']} {bench['unit']}, {bench['ms_per_step']} "
+          f"ms/step; trace: {len(timed)} dispatches in the timed region "
+          f"({per_step_n} per step)" if per_step_n else "(timed region not isolated)")
+    print(f"{'family':16s} {'trace ms/step':>14s} {'probe ms/step':>14s} {'ratio':>7s}")
+    for f in sorted(set(agg) | set(fams), key=lambda k: -agg.get(k, 0.0)):
+        t = agg.get(f, 0.0) / 1e6 / steps
+        pb = fams.get(f, {}).get("ms_per_step")
+        ratio = f"{pb / t:7.3f}" if pb and t else "      -"
+        print(f"{f:16s} {t:14.4f} {pb if pb is not None else '-':>14} {ratio}")
+
+
+if __name__ == "__main__":
+    main()
