@@ -78,15 +78,37 @@ def main():
             agg[f] += d
             if not f.startswith("reduce"):
                 last = f
+    # the probe steps themselves (eager launches between the first and the last empty launch):
+    # the same kernels bench.py's event pairs bracketed
+    last_probe = max((i for i, r in enumerate(rows) if "noop_kernel" in r[0]), default=-1)
+    pagg, pn = defaultdict(float), defaultdict(int)
+    last = None
+    for name, s, e, d in rows[first_probe:last_probe + 1]:
+        f = family(name)
+        if f == "reduce":
+            if last is not None:
+                pagg[last] += d
+            continue
+        if f is not None:
+            pagg[f] += d
+            pn[f] += 1
+            last = f
     print(f"bench: {bench['metric']}  {bench['value']} {bench['unit']}, {bench['ms_per_step']} "
           f"ms/step; trace: {len(timed)} dispatches in the timed region "
           f"({per_step_n} per step)" if per_step_n else "(timed region not isolated)")
-    print(f"{'family':16s} {'trace ms/step':>14s} {'probe ms/step':>14s} {'ratio':>7s}")
+    print(f"{'family':16s} {'timed region':>13s} {'probe':>9s} {'ratio':>6s} | "
+          f"{'probe-step trace':>17s} {'probe events':>13s} {'ratio':>6s}")
+    print(f"{'':16s} {'ms/step':>13s} {'ms/step':>9s} {'':>6s} | {'us/launch':>17s} "
+          f"{'us/launch':>13s}")
     for f in sorted(set(agg) | set(fams), key=lambda k: -agg.get(k, 0.0)):
         t = agg.get(f, 0.0) / 1e6 / steps
         pb = fams.get(f, {}).get("ms_per_step")
-        ratio = f"{pb / t:7.3f}" if pb and t else "      -"
-        print(f"{f:16s} {t:14.4f} {pb if pb is not None else '-':>14} {ratio}")
+        ratio = f"{pb / t:6.3f}" if pb and t else "     -"
+        tu = pagg[f] / pn[f] / 1e3 if pn.get(f) else None
+        eu = fams.get(f, {}).get("avg_launch_us")
+        r2 = f"{eu / tu:6.3f}" if tu and eu else "     -"
+        print(f"{f:16s} {t:13.4f} {pb if pb is not None else '-':>9} {ratio} | "
+              f"{(f'{tu:.2f}' if tu else '-'):>17s} {eu if eu is not None else '-':>13} {r2}")
 
 
 if __name__ == "__main__":
