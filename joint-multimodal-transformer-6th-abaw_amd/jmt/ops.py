@@ -179,7 +179,9 @@ def attn_fwd(dtype, N, H, Lq, Lk, dh, q_ptr, sq, k_ptr, sk, v_ptr, sv, o_ptr, so
     launch = lambda: _lib.call("jmt_attn_fwd", dtype, N, H, Lq, Lk, dh, q_ptr, sq[0], sq[1],
                                k_ptr, sk[0], sk[1], v_ptr, sv[0], sv[1], o_ptr, so[0], so[1],
                                scale, lse.data_ptr() if lse is not None else None, stream())
-    _hooked({"family": "attn_fwd", "flops": 4.0 * N * H * Lq * Lk * dh}, launch)
+    es = 4 if dtype == F32 else 2
+    _hooked({"family": "attn_fwd", "flops": 4.0 * N * H * Lq * Lk * dh,
+             "bytes": float(N * H) * ((2 * Lq + 2 * Lk) * dh * es + 4 * Lq)}, launch)
 
 
 def attn_bwd(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k_ptr, sk, v_ptr, sv,
@@ -190,8 +192,12 @@ def attn_bwd(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k_ptr, 
                                o_ptr, so[0], so[1], q_ptr, sq[0], sq[1], k_ptr, sk[0], sk[1],
                                v_ptr, sv[0], sv[1], lse.data_ptr(), p.data_ptr(), ds.data_ptr(),
                                ldp, dq_ptr, sdq[0], sdq[1], scale, stream())
-    # algorithmic: dP and dQ (the P recompute is not counted)
-    _hooked({"family": "attn_bwd", "flops": 4.0 * N * H * Lq * Lk * dh}, launch)
+    # algorithmic: dP and dQ (the P recompute is not counted); bytes: dO, O, Q, K, V, dQ, lse and
+    # the P / dS rows handed to the dK / dV products
+    es = 4 if dtype == F32 else 2
+    _hooked({"family": "attn_bwd", "flops": 4.0 * N * H * Lq * Lk * dh,
+             "bytes": float(N * H) * ((4 * Lq + 2 * Lk) * dh * es + 4 * Lq + 2 * Lq * ldp * es)},
+            launch)
 
 
 SMALL_ATTN_MAX_L = 8
