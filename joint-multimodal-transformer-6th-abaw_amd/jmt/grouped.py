@@ -201,6 +201,109 @@ def stack_joint(v, p, W, b) -> torch.Tensor:
     return StackJointFn.apply(v, p, W, b)
 
 
+class StackTokensFn(Function):
+    """The SELF_ATTEN head's token stack (mm_multi_transformers.py:171-178) from the stacked
+    cross-attention outputs O6 (S, B, T, E): a (B, T, S, E) buffer filled by S strided copies,
+    returned as its seq-first (S, B*T, E) view.  The backward writes dO6 (S, B, T, E) with S
+    strided copies — one gradient buffer, no per-slice zero-fill / copy / sum as the autograd of
+    S separate selections of O6 would run."""
+
+    @staticmethod
+    def forward(ctx, X):
+        cd = compute_dtype()
+        X = _contig(X, cd)
+        S, B, T, E = X.shape
+        buf = torch.empty(B, T, S, E, dtype=cd, device=X.device)
+        for s in range(S):
+            ops.copy2d(X[s].data_ptr(), ops.dt(X), _ptr(buf, s * E), ops.dt(buf), B * T, E, E, 1,
+                       S * E, 1)
+        ctx.meta = (S, B, T, E, cd)
+        return buf.view(B * T, S, E).permute(1, 0, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        S, B, T, E, cd = ctx.meta
+        gb = g.permute(1, 0, 2)                      # (B*T, S, E) logical
+        if gb.dtype != cd or gb.stride(2) != 1 or gb.stride(1) != E or gb.stride(0) != S * E:
+            gb = gb.to(cd).contiguous()
+        dX = torch.empty(S, B, T, E, dtype=cd, device=g.device)
+        for s in range(S):
+            ops.copy2d(_ptr(gb, s * E), ops.dt(gb), dX[s].data_ptr(), ops.dt(dX), B * T, E, S * E,
+                       1, E, 1)
+        return dX
+
+
+def stack_tokens(X) -> torch.Tensor:
+    return StackTokensFn.apply(X)
+
+
+class LastQueryMHAFn(Function):
+    """nn.MultiheadAttention(last, enc, enc) with last = enc[-1:] (the SELF_ATTEN head's final
+    attention, mm_multi_transformers.py:186-193: only the last query row is kept): q from the
+    last token's rows, packed k|v from all tokens, attention core, out_proj; returns (N, E).
+    The backward adds the query path's input gradient into the last token's rows of the key /
+    value path's input gradient with a beta = 1 GEMM epilogue — no zero-filled slice gradient
+    and no gradient sum."""
+
+    @staticmethod
+    def forward(ctx, enc, Win, bin_, Wout, bout, H):
+        from .functional import Rows, _ld, _linear_fwd
+        cd = compute_dtype()
+        L, N, E = enc.shape
+        X = Rows(enc, cd)                              # rows in enc's memory order
+        kv = X.like(2 * E, cd)
+        _linear_fwd([X.t], X.ld, X.rows, E, Win, E, 2 * E, bin_, kv, _ld(kv, X.perm), cd)
+        xl = X.t[-1:]
+        XL = Rows(xl)
+        q = XL.like(E, cd)
+        _linear_fwd([XL.t], XL.ld, XL.rows, E, Win, 0, E, bin_, q, _ld(q, XL.perm), cd)
+        o, asaved = attn_forward(q, kv, kv, E, H, 0, 0, E)
+        O = Rows(o)
+        y = O.like(E, cd)
+        _linear_fwd([O.t], O.ld, O.rows, E, Wout, 0, E, bout, y, _ld(y, O.perm), cd)
+        ctx.save_for_backward(X.t, q, kv, o, Win, bin_, Wout, bout)
+        ctx.asaved = asaved
+        ctx.meta = (cd, enc.dtype, X.perm, XL.perm, O.perm)
+        return y[0]
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .functional import (Rows, _bgrad, _cast_keep_layout, _dgrad, _ld, _match, _wgrad)
+        x, q, kv, o, Win, bin_, Wout, bout = ctx.saved_tensors
+        cd, xdt, xperm, xlperm, operm = ctx.meta
+        L, N, E = x.shape
+        O = Rows(o)
+        G = _match(gy.unsqueeze(0), Rows(O.like(E, cd)), cd)          # (1, N, E) in o's order
+        do = O.like(E, cd)
+        _dgrad(G, E, Wout, 0, cd, [do], _ld(do, O.perm), 1, E)
+        _wgrad(G, E, [O.t], O.ld, E, Wout, 0, cd)
+        _bgrad(G, E, bout, 0)
+        X = Rows(x)
+        dkv = X.like(2 * E, cd)
+        dq = Rows(q).like(E, cd)
+        attn_backward(ctx.asaved, do, dq, dkv, dkv)
+        DKV = Rows(dkv)
+        dx = X.like(E, cd)
+        _dgrad(DKV, 2 * E, Win, E, cd, [dx], _ld(dx, X.perm), 1, E)
+        _wgrad(DKV, 2 * E, [X.t], X.ld, E, Win, E, cd)
+        _bgrad(DKV, 2 * E, bin_, E)
+        DQ = Rows(dq)
+        XL = Rows(x[-1:])
+        dxl = dx[-1:]
+        _dgrad(DQ, E, Win, 0, cd, [dxl], _ld(dxl, XL.perm), 1, E, beta=1.0)
+        _wgrad(DQ, E, [XL.t], XL.ld, E, Win, 0, cd)
+        _bgrad(DQ, E, bin_, 0)
+        if xdt != cd:
+            dx = _cast_keep_layout(dx, xdt)
+        ctx.asaved = None
+        return dx, None, None, None, None, None
+
+
+def last_query_mha(enc, mha) -> torch.Tensor:
+    return LastQueryMHAFn.apply(enc, mha.in_proj_weight, mha.in_proj_bias, mha.out_proj.weight,
+                                mha.out_proj.bias, mha.num_heads)
+
+
 # ------------------------------------------------------------------------- encoder group
 def encoder_layer_params(layer) -> List[torch.Tensor]:
     """The 12 parameters of one TransformerEncoderLayer (mm_multi_transformers.py:48-70)."""

@@ -62,6 +62,14 @@ class TransformerEncoderLayer(nn.Module):
         self.layer_norm2 = LayerNorm(input_dim)
 
     def forward(self, x):
+        if grouped.enabled() and x.dim() == 3 and x.dtype == F.compute_dtype() and \
+                x.permute(1, 0, 2).is_contiguous():
+            # seq-first view of a (N, L, E) buffer (the SELF_ATTEN head's token stack, the
+            # ungrouped encoders): the grouped layer with one group — its backward accumulates
+            # the residual and projection input gradients in place (no autograd gradient sums)
+            Y = grouped.encoder_group(x.permute(1, 0, 2).unsqueeze(0), [self],
+                                      self.attention.num_heads)
+            return Y.squeeze(0).permute(1, 0, 2)
         attn_output, _ = self.attention(x, x, x)
         x = self.layer_norm1(x, attn_output)
         ff_output = self.feed_forward(x)
@@ -172,7 +180,9 @@ class MultimodalTransformer_w_JR(nn.Module):
                                           self.cross_attention_pv], self.num_heads)
         taps.record_stacked([f"ca.{i}" for i in range(O6.shape[0])], O6)
         if self.output_format == "SELF_ATTEN":
-            return self._self_atten_head([O6[i].permute(1, 0, 2) for i in range(6)])
+            S, B, T, E = O6.shape
+            enc = self.final_visual_encoder(grouped.stack_tokens(O6))
+            return grouped.last_query_mha(enc, self.final_self_attention).reshape(B, T, E)
         # FC head (:201-211): seq-first (T, B, 1024), as the reference returns it
         return grouped.concat_linear(O6, self.out_layer1.weight,
                                      self.out_layer1.bias).permute(1, 0, 2)
@@ -184,9 +194,7 @@ class MultimodalTransformer_w_JR(nn.Module):
         T, B, E = outs[0].shape
         st = F.stack_seq(outs, seq_first_in=True)
         enc = self.final_visual_encoder(st)
-        last = enc[-1:]
-        fa, _ = self.final_self_attention(last, enc, enc)
-        return fa[0].reshape(B, T, E)
+        return grouped.last_query_mha(enc, self.final_self_attention).reshape(B, T, E)
 
 
 class FeatureConcatFC(nn.Module):
