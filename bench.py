@@ -271,6 +271,8 @@ def main():
                     help="eager launches from Python every step")
     ap.add_argument("--probe-steps", type=int, default=3)
     ap.add_argument("--launch-log", default=None, help="write per-launch records (jsonl)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: B windows per GPU (headline); strong: B windows in total")
     ap.add_argument("--bucket-mb", type=int, default=8,
                     help="gradient all-reduce bucket size (MiB) for N > 1")
     ap.add_argument("--no-overlap", action="store_true",
@@ -334,6 +336,11 @@ def main():
     args.dtype = args.dtype or cfg["dtype"]
     cd = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
     B = args.batch or cfg["B"]
+    if args.scaling == "strong":
+        # fixed GLOBAL batch (SURVEY.md §8e strong scaling): each rank takes its contiguous share
+        if B % world:
+            raise SystemExit(f"--scaling strong: global batch {B} not divisible by {world} ranks")
+        B //= world
     T = args.seq or cfg["T"]
     Da, Dv = cfg["Da"], cfg["Dv"]
     fl_kw = dict(Da=Da, Dv=Dv, fc=cfg["fc"], jm=cfg["jm"], fmt=cfg["fmt"], k=k)
@@ -349,11 +356,19 @@ def main():
         jdist.set_loss_group(dist.group.WORLD)
 
     # synthetic inputs resident in HBM, disjoint per rank (global batch = world * B)
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    audio = torch.randn(B, T, Da, device=dev, generator=g)
-    video = torch.randn(B, T, Dv, device=dev, generator=g)
-    lv = (torch.rand(B, T, device=dev, generator=g) * 2 - 1).view(-1, B * T)
-    la = (torch.rand(B, T, device=dev, generator=g) * 2 - 1).view(-1, B * T)
+    # one generator per GLOBAL window index: rank r holds windows
+    # [r*B, (r+1)*B), so the 1/2/4/8-GPU runs see identical global batches
+    audio = torch.empty(B, T, Da, device=dev)
+    video = torch.empty(B, T, Dv, device=dev)
+    lv = torch.empty(B, T, device=dev)
+    la = torch.empty(B, T, device=dev)
+    for i in range(B):
+        g = torch.Generator(device=dev).manual_seed(1000 + rank * B + i)
+        audio[i].normal_(generator=g)
+        video[i].normal_(generator=g)
+        lv[i].uniform_(-1.0, 1.0, generator=g)
+        la[i].uniform_(-1.0, 1.0, generator=g)
+    lv, la = lv.view(-1, B * T), la.view(-1, B * T)
     crit = CCCLoss(k)
     # k = 1: train.py:303-307's (1, T*B) views; k > 1 (c5's expression-style head): the (T, B, k)
     # logits as the (N, k) rows loss.py:18-22 takes, labels (N,)
@@ -496,7 +511,7 @@ def main():
             "metric": "train windows/sec + CCC parity, B=64 T=300 A/V fusion, 1/2/4/8 MI355X",
             "value": round(value, 2), "unit": "windows/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": args.dtype, "data": "synthetic (N(0,1) features, U(-1,1) labels, "
                                          "random-init weights)",
             "config": {"workload": cfg["desc"],
