@@ -118,6 +118,17 @@ int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, int D, cons
                       int64_t lddx, float* dgamma, float* dbeta, int beta_acc, float* partials,
                       void* stream);
 
+/* jmt_layernorm_bwd plus dsum (+)= the column sums of dx (the gradient of the bias of the linear
+ * whose output entered the residual sum: FFN out / attention out_proj, mm_multi_transformers.py:
+ * 52-70), reduced with dgamma / dbeta (partials: 3 * D * jmt_layernorm_bwd_blocks(rows) floats,
+ * 16-B aligned).  D in {512, 768, 1024} with 4-element aligned rows; otherwise returns
+ * JMT_ERR_UNSUPPORTED and writes nothing. */
+int jmt_layernorm_bwd_dsum(int dt_in, int dt_dy, int dt_dx, int64_t rows, int D, const void* x,
+                           int64_t ldx, const void* r, int64_t ldr, const void* dy, int64_t lddy,
+                           const float* mean, const float* rstd, const float* gamma, void* dx,
+                           int64_t lddx, float* dgamma, float* dbeta, float* dsum, int beta_acc,
+                           float* partials, void* stream);
+
 /* Attention softmax (F.multi_head_attention_forward): rows of length n of the
  * fp32 score matrix S (ld) -> P = softmax(scale * S) stored as p_dt at ldp; columns [n, ldp)
  * of P are zeroed. */

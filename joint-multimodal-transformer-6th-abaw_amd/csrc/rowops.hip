@@ -230,23 +230,24 @@ __global__ __launch_bounds__(RB) void ln_fwd_vec_kernel(int64_t rows, const TI* 
 }
 
 // NV = D / 256: lane owns elements 4*(lane + 64 j) .. +3, j < NV
-template <typename TI, typename TG, typename TD, int NV>
+template <typename TI, typename TG, typename TD, int NV, bool DS = false>
 __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* x, int64_t ldx,
                                                         const TI* rr, int64_t ldr, const TG* dy,
                                                         int64_t lddy, const float* mean,
                                                         const float* rstd, const float* gamma,
                                                         TD* dx, int64_t lddx, float* partials) {
   constexpr int D = NV * 256;
-  __shared__ float red[4][2][D];
+  constexpr int NS = DS ? 3 : 2;                 // slabs: dgamma, dbeta (+ column sums of dx)
+  __shared__ float red[4][NS][D];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  float pg[NV][4], pb[NV][4], gm[NV][4];
+  float pg[NV][4], pb[NV][4], gm[NV][4], ps[NV][4];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const float4 g4 = *(const float4*)(gamma + 4 * (lane + 64 * j));
     gm[j][0] = g4.x; gm[j][1] = g4.y; gm[j][2] = g4.z; gm[j][3] = g4.w;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) pg[j][e] = pb[j][e] = 0.f;
+    for (int e = 0; e < 4; ++e) pg[j][e] = pb[j][e] = ps[j][e] = 0.f;
   }
   const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK;
   for (int i = w; i < LN_ROWS_PER_BLOCK; i += 4) {
@@ -285,6 +286,10 @@ __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* 
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = rs * (gd[j][e] - s1 - xh[j][e] * s2);
       V4<TD>::st(dx + r * lddx + 4 * (lane + 64 * j), o);
+      if constexpr (DS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ps[j][e] += o[e];
+      }
     }
   }
 #pragma unroll
@@ -293,10 +298,11 @@ __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* 
     for (int e = 0; e < 4; ++e) {
       red[w][0][4 * (lane + 64 * j) + e] = pg[j][e];
       red[w][1][4 * (lane + 64 * j) + e] = pb[j][e];
+      if constexpr (DS) red[w][2][4 * (lane + 64 * j) + e] = ps[j][e];
     }
   __syncthreads();
-  float* out = partials + (int64_t)blockIdx.x * 2 * D;
-  for (int c = threadIdx.x; c < 2 * D; c += RB) {
+  float* out = partials + (int64_t)blockIdx.x * NS * D;
+  for (int c = threadIdx.x; c < NS * D; c += RB) {
     const int h = c / D, cc = c - h * D;
     out[c] = red[0][h][cc] + red[1][h][cc] + red[2][h][cc] + red[3][h][cc];
   }
@@ -372,7 +378,8 @@ struct OutTab { float* p[8]; };
 __global__ __launch_bounds__(RB) void slab_reduce_kernel(int nblk, int W, const float* partials,
                                                          int64_t stride, int split, float* out0,
                                                          float* out1, int beta_acc,
-                                                         OutTab tab = OutTab{}, int grouped = 0) {
+                                                         OutTab tab = OutTab{}, int grouped = 0,
+                                                         float* out2 = nullptr) {
   if (grouped) {   // group g = blockIdx.y: slabs at partials + g*nblk*stride, output tab.p[g]
     partials += (int64_t)blockIdx.y * nblk * stride;
     out0 = out1 = tab.p[blockIdx.y];
@@ -426,7 +433,8 @@ __global__ __launch_bounds__(RB) void slab_reduce_kernel(int nblk, int W, const 
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int col = cc + e;
-      float* o = col < split ? out0 + col : out1 + (col - split);
+      float* o = col < split ? out0 + col
+                 : (out2 && col >= 2 * split) ? out2 + (col - 2 * split) : out1 + (col - split);
       *o = beta_acc ? *o + tv[e] : tv[e];
     }
   }
@@ -753,6 +761,42 @@ extern "C" int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, 
   JMT_LAUNCH_CHECK("jmt_layernorm_bwd");
   launch_slab_reduce(nblk, 2 * D, partials, (int64_t)2 * D, D, dgamma, dbeta, beta_acc, st);
   JMT_LAUNCH_CHECK("jmt_layernorm_bwd(reduce)");
+  return JMT_OK;
+}
+
+extern "C" int jmt_layernorm_bwd_dsum(int dt_in, int dt_dy, int dt_dx, int64_t rows, int D,
+                                      const void* x, int64_t ldx, const void* r, int64_t ldr,
+                                      const void* dy, int64_t lddy, const float* mean,
+                                      const float* rstd, const float* gamma, void* dx,
+                                      int64_t lddx, float* dgamma, float* dbeta, float* dsum,
+                                      int beta_acc, float* partials, void* stream) {
+  if (rows == 0) return JMT_OK;
+  JMT_CHECK_ARG(x && dy && dx && mean && rstd && gamma && partials && dgamma && dbeta && dsum,
+                "jmt_layernorm_bwd_dsum: null pointer");
+  const bool vec = (D == 512 || D == 768 || D == 1024) && (ldx % 4 == 0) && (lddy % 4 == 0) &&
+                   (lddx % 4 == 0) && (!r || ldr % 4 == 0) && ((uintptr_t)gamma % 16 == 0) &&
+                   ((uintptr_t)x % (4 * dtype_size(dt_in)) == 0) &&
+                   ((uintptr_t)r % (4 * dtype_size(dt_in)) == 0) &&
+                   ((uintptr_t)dy % (4 * dtype_size(dt_dy)) == 0) &&
+                   ((uintptr_t)dx % (4 * dtype_size(dt_dx)) == 0) &&
+                   ((uintptr_t)partials % 16 == 0);
+  if (!vec)
+    return set_error(JMT_ERR_UNSUPPORTED, "jmt_layernorm_bwd_dsum: D=%d / layout not covered", D);
+  hipStream_t st = as_stream(stream);
+  const int nblk = jmt_layernorm_bwd_blocks(rows);
+#define JMT_LNB_DS(NV)                                                                          \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV, true>), dim3(nblk), dim3(RB), 0, st, rows, \
+                     (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd,    \
+                     gamma, (TD*)dx, lddx, partials)
+  JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_dy, TG, JMT_DISPATCH1(dt_dx, TD,
+      if (D == 512) { JMT_LNB_DS(2); }
+      else if (D == 768) { JMT_LNB_DS(3); }
+      else { JMT_LNB_DS(4); })));
+#undef JMT_LNB_DS
+  JMT_LAUNCH_CHECK("jmt_layernorm_bwd_dsum");
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((3 * D + 15) / 16), dim3(RB), 0, st, nblk, 3 * D,
+                     partials, (int64_t)3 * D, D, dgamma, dbeta, beta_acc, OutTab{}, 0, dsum);
+  JMT_LAUNCH_CHECK("jmt_layernorm_bwd_dsum(reduce)");
   return JMT_OK;
 }
 

@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libjmt_hip.so")
 
 F32, BF16, F16 = 0, 1, 2
+OK, ERR_ARG, ERR_HIP, ERR_UNSUPPORTED = 0, -1, -2, -3     # include/jmt.h
 
 c_i64 = C.c_int64
 c_vp = C.c_void_p
@@ -62,6 +63,9 @@ _PROTOS = {
     "jmt_layernorm_bwd": (c_int, [c_int, c_int, c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_i64,
                                   c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_int,
                                   c_vp, c_vp]),
+    "jmt_layernorm_bwd_dsum": (c_int, [c_int, c_int, c_int, c_i64, c_int, c_vp, c_i64, c_vp,
+                                       c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
+                                       c_vp, c_vp, c_int, c_vp, c_vp]),
     "jmt_softmax_fwd": (c_int, [c_int, c_i64, c_int, c_vp, c_i64, c_f, c_vp, c_i64, c_vp]),
     "jmt_softmax_bwd": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_i64, c_f, c_vp,
                                 c_i64, c_vp]),

@@ -373,28 +373,43 @@ class EncoderGroupFn(Function):
         cdt = _dc(cd)
         dY = _contig(dY, cd)
 
-        def ln_bwd(x, r, dy, st, gamma, beta, dx):
+        def ln_bwd(x, r, dy, st, gamma, beta, dx, bias=None):
+            """LayerNorm backward per group; with `bias` (the biases of the linears whose
+            outputs r entered the residual sums) their gradients — the column sums of dx — are
+            reduced in the same launch pair.  Returns whether they were."""
+            fused = bias is not None
             for g in range(G):
                 dgam = _grad_buffer(gamma[g])
                 dbet = _grad_buffer(beta[g])
+                dbias = _grad_buffer(bias[g]) if bias is not None else None
                 tmp = None
-                if dgam is None or dbet is None:
-                    tmp = torch.empty(2, E, dtype=torch.float32, device=dev)
-                ops.layernorm_bwd(x[g], E, r[g], E, dy[g], E, st[0, g * R:], st[1, g * R:],
-                                  gamma[g], dx[g], E, dgam if dgam is not None else tmp[0],
-                                  dbet if dbet is not None else tmp[1], tmp is None, R, E)
+                if dgam is None or dbet is None or (bias is not None and dbias is None):
+                    tmp = torch.empty(3, E, dtype=torch.float32, device=dev)
+                args = (x[g], E, r[g], E, dy[g], E, st[0, g * R:], st[1, g * R:], gamma[g], dx[g],
+                        E, dgam if dgam is not None else tmp[0],
+                        dbet if dbet is not None else tmp[1])
+                if fused and ops.layernorm_bwd_dsum(
+                        *args, dbias if dbias is not None else tmp[2], tmp is None, R, E) is not None:
+                    _grad_done(gamma[g], beta[g], bias[g])
+                    continue
+                ops.layernorm_bwd(*args, tmp is None, R, E)
                 _grad_done(gamma[g], beta[g])
+                if fused:        # shape not covered by the fused form: this group's bias apart
+                    _bias_grad(dx[g].view(R, E), E, R, E, bias[g], 0)
+            return fused
 
         # LN2: dS2 = d(H1 + F2)
         dS = torch.empty(G, B, T, E, dtype=cd, device=dev)
-        ln_bwd(H1, F2, dY, st2, [p[10] for p in P], [p[11] for p in P], dS)
+        b2_done = ln_bwd(H1, F2, dY, st2, [p[10] for p in P], [p[11] for p in P], dS,
+                         bias=[p[7] for p in P])
         # FFN (the ReLU mask is fused into the W2 dgrad epilogue)
         dF1 = torch.empty(G, B, T, hid, dtype=cd, device=dev)
         _gemm_dgrad(dS.data_ptr(), E, R * E, R, E, [p[6] for p in P], 0, dF1.data_ptr(), hid,
                     R * hid, cdt, cd, dev, aux=F1, ldaux=hid)
         _gemm_wgrad([dS.data_ptr()], E, R * E, [F1.data_ptr()], hid, R * hid, R, E,
                     [p[6] for p in P], 0, cd, dev)
-        _bias_grad_grouped(dS.data_ptr(), G, E, R * E, R, E, [p[7] for p in P], 0, cd, dev)
+        if not b2_done:
+            _bias_grad_grouped(dS.data_ptr(), G, E, R * E, R, E, [p[7] for p in P], 0, cd, dev)
         # dH1 = dS2 + dF1 . W1  (in place on dS: beta = 1)
         _gemm_dgrad(dF1.data_ptr(), hid, R * hid, R, hid, [p[4] for p in P], 0, dS.data_ptr(),
                     E, R * E, cdt, cd, dev, beta=1.0)
@@ -404,14 +419,16 @@ class EncoderGroupFn(Function):
                            dev)
         # LN1: dS1 = d(X + A1)
         dS1 = torch.empty_like(dS)
-        ln_bwd(X, A1, dS, st1, [p[8] for p in P], [p[9] for p in P], dS1)
+        bo_done = ln_bwd(X, A1, dS, st1, [p[8] for p in P], [p[9] for p in P], dS1,
+                         bias=[p[3] for p in P])
         # out_proj
         dO = dS     # reuse: dS is dead
         _gemm_dgrad(dS1.data_ptr(), E, R * E, R, E, [p[2] for p in P], 0, dO.data_ptr(), E,
                     R * E, cdt, cd, dev)
         _gemm_wgrad([dS1.data_ptr()], E, R * E, [O.data_ptr()], E, R * E, R, E,
                     [p[2] for p in P], 0, cd, dev)
-        _bias_grad_grouped(dS1.data_ptr(), G, E, R * E, R, E, [p[3] for p in P], 0, cd, dev)
+        if not bo_done:
+            _bias_grad_grouped(dS1.data_ptr(), G, E, R * E, R, E, [p[3] for p in P], 0, cd, dev)
         # attention core -> packed dQKV
         dQKV = torch.empty(G, B, T, 3 * E, dtype=cd, device=dev)
         dsf = dQKV.view(G * B, T, 3 * E).permute(1, 0, 2)

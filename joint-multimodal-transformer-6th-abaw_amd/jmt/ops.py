@@ -146,6 +146,23 @@ def layernorm_bwd(x, ldx, r, ldr, dy, lddy, mean, rstd, gamma, dx, lddx, dgamma,
     return part
 
 
+def layernorm_bwd_dsum(x, ldx, r, ldr, dy, lddy, mean, rstd, gamma, dx, lddx, dgamma, dbeta,
+                       dsum, beta_acc, rows, D):
+    """layernorm_bwd plus dsum (+)= column sums of dx; returns the partials buffer, or None when
+    the shape is not covered (nothing written: the caller reduces dsum itself)."""
+    nblk = _lib.load().jmt_layernorm_bwd_blocks(rows)
+    part = torch.empty(max(nblk, 1) * 3 * D, dtype=torch.float32, device=x.device)
+    rc = _lib.load().jmt_layernorm_bwd_dsum(
+        dt(x), dt(dy), dt(dx), rows, D, x.data_ptr(), ldx,
+        r.data_ptr() if r is not None else None, ldr, dy.data_ptr(), lddy, mean.data_ptr(),
+        rstd.data_ptr(), gamma.data_ptr(), dx.data_ptr(), lddx, dgamma.data_ptr(),
+        dbeta.data_ptr(), dsum.data_ptr(), int(beta_acc), part.data_ptr(), stream())
+    if rc == _lib.ERR_UNSUPPORTED:
+        return None
+    _lib.check(rc, "jmt_layernorm_bwd_dsum")
+    return part
+
+
 def softmax_fwd(s, lds, rows, n, scale, p, ldp):
     _lib.call("jmt_softmax_fwd", dt(p), rows, n, s.data_ptr(), lds, scale, p.data_ptr(), ldp,
               stream())

@@ -641,3 +641,41 @@ def test_short_sequences_dispatch_to_small_attn(cd):
     tol = 1e-5 if cd == torch.float32 else 2e-2
     for a, b in zip(*outs):
         assert (a - b).abs().max().item() <= tol * b.abs().max().item()
+
+
+@pytest.mark.parametrize("D", [512, 768])
+def test_layernorm_bwd_dsum_matches_colsum(D):
+    """jmt_layernorm_bwd_dsum: dx, dgamma, dbeta as jmt_layernorm_bwd and dsum (+)= the
+    fp32 column sums of dx (the residual branch's bias gradient), accumulated onto dsum."""
+    cd = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(31)
+    rows = 1000
+    x = torch.randn(rows, D, device=DEV, generator=g).to(cd)
+    r = torch.randn(rows, D, device=DEV, generator=g).to(cd)
+    dy = torch.randn(rows, D, device=DEV, generator=g).to(cd)
+    gamma = torch.randn(D, device=DEV, generator=g)
+    beta = torch.randn(D, device=DEV, generator=g)
+    y = torch.empty(rows, D, dtype=cd, device=DEV)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    ops.layernorm_fwd(x, D, r, D, gamma, beta, 1e-5, y, D, mean, rstd, rows, D)
+    outs = []
+    for fused in (False, True):
+        dx = torch.empty(rows, D, dtype=cd, device=DEV)
+        dg = torch.full((D,), 0.5, device=DEV)
+        db = torch.full((D,), 0.25, device=DEV)
+        ds = torch.full((D,), 1.0, device=DEV)
+        if fused:
+            assert ops.layernorm_bwd_dsum(x, D, r, D, dy, D, mean, rstd, gamma, dx, D, dg, db, ds,
+                                          True, rows, D) is not None
+        else:
+            ops.layernorm_bwd(x, D, r, D, dy, D, mean, rstd, gamma, dx, D, dg, db, True, rows, D)
+        torch.cuda.synchronize()
+        outs.append((dx, dg, db, ds))
+    (dx0, dg0, db0, _), (dx1, dg1, db1, ds1) = outs
+    # the two instantiations may contract the dx arithmetic differently: 1 bf16 ulp apart at most
+    assert (dx0.float() - dx1.float()).abs().max().item() <= 2.0 ** -7 * dx0.float().abs().max().item()
+    assert torch.allclose(dg0, dg1, rtol=1e-5, atol=1e-4) and torch.allclose(db0, db1, rtol=1e-5,
+                                                                              atol=1e-4)
+    want = 1.0 + dx0.float().sum(0)
+    assert (ds1 - want).abs().max().item() <= 1e-2 * want.abs().max().item() + 1e-3
