@@ -105,6 +105,9 @@ using Cfg21 = TileCfg<128, 128, 2, 2, 64, 4, 1, 1, 0, 2, 1>;
 // r02_hipblaslt_reference.txt — compiled without spills but measured 1.45-1.65x slower than
 // Cfg5 / Cfg20 on every step shape, with and without interleaved DMA issue: one wave per SIMD
 // leaves each wave's LDS-read latency exposed; profiles/r02_gemm_4wave_256.txt)
+// (4-wave 256x128 / 128x256 tiles — a wave 128x64 / 64x128, 64-B K-tiles, 3 stages, 2 blocks /
+// CU so one block's epilogue burst overlaps the other's K loop — measured 0-30 % slower than the
+// chosen configs on every step shape: profiles/r02_gemm_4wave_rect.jsonl)
 // (without s_setprio the two measured the same: profiles/r01_gemm_occupancy.txt)
 // (8-wave 128x256 / 256x128 tiles with 64-B K-tiles, 3 stages, 2 blocks / CU measured 20-100%
 // slower on every step shape: profiles/r01_gemm_occupancy.txt)
