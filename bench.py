@@ -59,6 +59,24 @@ CONFIGS = {
 }
 
 
+def synthetic_batch(B: int, T: int, Da: int, Dv: int, rank: int, dev):
+    """Rank `rank`'s B windows of synthetic data: audio / video ~ N(0,1), labels ~ U(-1,1), one
+    generator per GLOBAL window index, so rank r holds windows [r*B, (r+1)*B)
+    and the 1/2/4/8-GPU runs see identical global batches.  Labels come as the (1, B*T) views
+    train.py:303-307 makes."""
+    audio = torch.empty(B, T, Da, device=dev)
+    video = torch.empty(B, T, Dv, device=dev)
+    lv = torch.empty(B, T, device=dev)
+    la = torch.empty(B, T, device=dev)
+    for i in range(B):
+        g = torch.Generator(device=dev).manual_seed(1000 + rank * B + i)
+        audio[i].normal_(generator=g)
+        video[i].normal_(generator=g)
+        lv[i].uniform_(-1.0, 1.0, generator=g)
+        la[i].uniform_(-1.0, 1.0, generator=g)
+    return audio, video, lv.view(-1, B * T), la.view(-1, B * T)
+
+
 def step_flops(B: int, T: int, Da: int = D_A, Dv: int = D_V, fc: bool = True,
                jm: str = "TRANSFORMER", fmt: str = "FC", k: int = 1):
     """Algorithmic matmul FLOPs of one training step (SURVEY.md §8d closed form for
@@ -356,19 +374,7 @@ def main():
         jdist.set_loss_group(dist.group.WORLD)
 
     # synthetic inputs resident in HBM, disjoint per rank (global batch = world * B)
-    # one generator per GLOBAL window index: rank r holds windows
-    # [r*B, (r+1)*B), so the 1/2/4/8-GPU runs see identical global batches
-    audio = torch.empty(B, T, Da, device=dev)
-    video = torch.empty(B, T, Dv, device=dev)
-    lv = torch.empty(B, T, device=dev)
-    la = torch.empty(B, T, device=dev)
-    for i in range(B):
-        g = torch.Generator(device=dev).manual_seed(1000 + rank * B + i)
-        audio[i].normal_(generator=g)
-        video[i].normal_(generator=g)
-        lv[i].uniform_(-1.0, 1.0, generator=g)
-        la[i].uniform_(-1.0, 1.0, generator=g)
-    lv, la = lv.view(-1, B * T), la.view(-1, B * T)
+    audio, video, lv, la = synthetic_batch(B, T, Da, Dv, rank, dev)
     crit = CCCLoss(k)
     # k = 1: train.py:303-307's (1, T*B) views; k > 1 (c5's expression-style head): the (T, B, k)
     # logits as the (N, k) rows loss.py:18-22 takes, labels (N,)

@@ -1,6 +1,9 @@
 """Host-side logic of the drop-in modules that needs no GPU: module/class identity, constructor
 signatures, state_dict keys and shapes identical to the reference, layout bookkeeping."""
 import inspect
+import os
+
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 import pytest
 import torch
@@ -120,3 +123,17 @@ def test_compute_dtype_policy():
     with F.compute_mode(torch.bfloat16):
         assert F.compute_dtype() == torch.bfloat16
     assert F.compute_dtype() == torch.float32
+
+
+def test_bench_synthetic_batches_identical_across_world_sizes():
+    """bench.py's per-global-window generators: 2 ranks x 3 windows == 1 rank x 6 windows."""
+    import importlib
+    import sys
+    sys.path.insert(0, REPO_ROOT)
+    bench = importlib.import_module("bench")
+    one = bench.synthetic_batch(6, 5, 8, 16, 0, "cpu")
+    two = [bench.synthetic_batch(3, 5, 8, 16, r, "cpu") for r in range(2)]
+    for k in range(2):                                    # audio, video
+        assert torch.equal(one[k], torch.cat([two[0][k], two[1][k]], 0))
+    for k in range(2, 4):                                 # labels (1, B*T)
+        assert torch.equal(one[k].view(6, 5), torch.cat([t[k].view(3, 5) for t in two], 0))
