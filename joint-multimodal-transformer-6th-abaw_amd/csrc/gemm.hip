@@ -987,6 +987,9 @@ static bool tile_ok(const TileModel& t, int M, int N) {
 static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, int splits) {
   if (!ak && !bk && M >= 1536 && N >= 512 && batch >= 3 && K >= 8192)
     return 10;                                                   // split-K qkv wgrad
+  if (!ak && !bk && batch == 6 && M == 1024 && N == 512 && K >= 8192)
+    return 5;          // cross-attention k|v wgrad: 256x256 at the planner's splits (-8 %,
+                       // profiles/r02_wgrad_splits_b6.jsonl)
   if (splits > 1) return 0;
   if (!ak && !bk && batch >= 64 && M <= 512 && N <= 512 && K >= 128 && K <= 512)
     return 11;                                                   // attn dK / dV

@@ -33,6 +33,9 @@ def make_shapes(R):
         ("wgrad b3 TN 512x512xR", 512, 512, R, False, False, 3, F32, {"beta": 1.0}),
         ("wgrad b3 TN 1536x512xR", 1536, 512, R, False, False, 3, F32, {"beta": 1.0}),
         ("attn dKdV b384 TN 300x512x300", 300, 512, 300, False, False, 384, BF16, {}),
+        ("ca wgrad b6 TN 1024x512xR", 1024, 512, R, False, False, 6, F32, {"beta": 1.0}),
+        ("ca wgrad b6 TN 512x512xR", 512, 512, R, False, False, 6, F32, {"beta": 1.0}),
+        ("enc wgrad b3 TN 512x1536xR", 512, 1536, R, False, False, 3, F32, {"beta": 1.0}),
     ]
 
 
