@@ -108,6 +108,10 @@ using Cfg21 = TileCfg<128, 128, 2, 2, 64, 4, 1, 1, 0, 2, 1>;
 // (4-wave 256x128 / 128x256 tiles — a wave 128x64 / 64x128, 64-B K-tiles, 3 stages, 2 blocks /
 // CU so one block's epilogue burst overlaps the other's K loop — measured 0-30 % slower than the
 // chosen configs on every step shape: profiles/r02_gemm_4wave_rect.jsonl)
+// (64x64 tiles — 4 waves of 32x32, 128-B K-tiles, 8 stages: a whole K = 512 reduction in flight —
+// for the few-tile T=16 real-data launches measured 0-10 % slower than the 128x128 tile there, and
+// up to 2x slower on larger launches: those launches sit on a ~15 us floor of launch, first-load
+// and store-drain latency, not on per-K-tile latency; profiles/r02_gemm_small_tiles_realdata.jsonl)
 // (without s_setprio the two measured the same: profiles/r01_gemm_occupancy.txt)
 // (8-wave 128x256 / 256x128 tiles with 64-B K-tiles, 3 stages, 2 blocks / CU measured 20-100%
 // slower on every step shape: profiles/r01_gemm_occupancy.txt)
@@ -138,7 +142,12 @@ __device__ __forceinline__ int swz_k(int row) {
   if constexpr (KB == 128) return (row >> 1) & 7;
   else return (row >> 2) & 3;
 }
-__device__ __forceinline__ int swz_t(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+// (an MN-major k-row of RB bytes holds RB/32 pairs of 16-B chunks: the XOR stays inside it)
+template <int RB>
+__device__ __forceinline__ int swz_t(int k) {
+  if constexpr (RB >= 256) return (k & 3) | (((k >> 3) & 1) << 2);
+  else return (k & 3) & (RB / 32 - 1);
+}
 
 // Physical 16-B chunk `id` (image byte id*16) -> its logical source element (row index in the
 // M/N dimension, k index) of one K-tile.  Shared by the LDS-DMA and the register paths, whose LDS
@@ -155,7 +164,8 @@ __device__ __forceinline__ void chunk_src(int id, int& row, int& kk) {
     constexpr int CPR = ROWS * (int)sizeof(T) / 16;
     kk = id / CPR;
     const int cp = id % CPR;
-    const int c = (sizeof(T) == 2) ? ((((cp >> 1) ^ swz_t(kk)) << 1) | (cp & 1)) : cp;
+    const int c = (sizeof(T) == 2) ? ((((cp >> 1) ^ swz_t<ROWS * (int)sizeof(T)>(kk)) << 1) | (cp & 1))
+                                   : cp;
     row = c * V;
   }
 }
@@ -282,7 +292,7 @@ __device__ __forceinline__ int kmaj_off(int row, int c) {
 template <int RB>
 __device__ __forceinline__ int mnmaj16_off(int k, int m) {
   const int c = m >> 3;
-  const int cp = ((((c >> 1) ^ swz_t(k))) << 1) | (c & 1);
+  const int cp = ((((c >> 1) ^ swz_t<RB>(k))) << 1) | (c & 1);
   return k * RB + (cp << 4) + ((m & 7) << 1);
 }
 
@@ -432,14 +442,20 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n) for sma
   }
 }
 
-// wait until at most n (runtime, < 4) K-tiles of VMT DMA instructions each are outstanding
+// wait until at most n (runtime, < 8) K-tiles of VMT DMA instructions each are outstanding
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_capped() { wait_vmcnt<(N < 63 ? N : 63)>(); }
 template <int VMT>
 __device__ __forceinline__ void wait_tiles(int n) {
   switch (n) {
     case 0: wait_vmcnt<0>(); break;
-    case 1: wait_vmcnt<VMT>(); break;
-    case 2: wait_vmcnt<2 * VMT>(); break;
-    default: wait_vmcnt<3 * VMT>(); break;
+    case 1: wait_vmcnt_capped<VMT>(); break;
+    case 2: wait_vmcnt_capped<2 * VMT>(); break;
+    case 3: wait_vmcnt_capped<3 * VMT>(); break;
+    case 4: wait_vmcnt_capped<4 * VMT>(); break;
+    case 5: wait_vmcnt_capped<5 * VMT>(); break;
+    case 6: wait_vmcnt_capped<6 * VMT>(); break;
+    default: wait_vmcnt_capped<7 * VMT>(); break;
   }
 }
 
@@ -797,7 +813,7 @@ void gemm_kernel(GemmParams p) {
   } else {
     // S-1 tiles in flight, one barrier per tile: the barrier of iteration kt also certifies that
     // every wave finished computing tile kt-1, whose buffer receives tile kt+S-1.
-    static_assert(C::S <= 5, "wait_tiles covers up to 3 newer tiles");
+    static_assert(C::S <= 9 && (C::S - 2) * VMT < 64, "wait_tiles covers up to 7 newer tiles");
 #pragma unroll
     for (int i = 0; i < C::S - 1; ++i)
       if (i < nfull) issue_ktile<T, AK, BK, C>(p, smem, cur, i, i);
