@@ -64,7 +64,8 @@ struct GemmParams {
   int tiles_m, tiles_n;
   int c_vec4;                   // C (and aux) 4-element groups aligned for 4-element stores
   int c_vec8;                   // C rows / base 16-B aligned (16-bit C: paired 16-B stores)
-  int dbg;                      // development ablations: 1 skip MFMA, 2 skip epilogue, 8 trace
+  int dbg;                      // development ablations: 1 skip MFMA, 2 skip epilogue, 8 trace,
+                                //   16 split-K work dealt per (batch, split) as without splits
 };
 
 // PF: A-fragment prefetch distance in MFMA rows; PRIO: s_setprio(1) around each MFMA row;
@@ -489,6 +490,17 @@ template <class C>
 __device__ __forceinline__ GemmWork decode_work(const GemmParams& p, int w) {
   const int ntile = p.tiles_m * p.tiles_n;
   const int nb = p.batch0 * p.batch1;
+  // split-K: every tile of one (batch entry, K split) reads the same K rows of both operands, so
+  // the whole work list is remapped (bijectively) so that each XCD — the hardware deals blocks
+  // to XCDs round-robin by linear id — runs a contiguous range of work items, i.e. whole
+  // (batch, split) groups whose operand rows its own L2 serves to all of the group's tiles
+  // (dealt across the XCDs, each group's operand panels were fetched ~3x from HBM / MALL)
+  const bool global = p.splits > 1 && !(p.dbg & 16);
+  if (global) {
+    const int W = ntile * nb * p.splits;
+    const int q = W / 8, rm = W % 8, x = w % 8;
+    w = x * q + min(x, rm) + w / 8;
+  }
   const int bid = w % ntile;
   const int rest = w / ntile;
   GemmWork r;
@@ -496,7 +508,7 @@ __device__ __forceinline__ GemmWork decode_work(const GemmParams& p, int w) {
   r.split = rest / nb;
   // XCD-aware remap (bijective): consecutive logical tiles (same A row panel) on one XCD.
   int wg = bid;
-  if (ntile >= 16) {
+  if (!global && ntile >= 16) {
     const int q = ntile / 8, rm = ntile % 8, x = bid % 8;
     wg = (x < rm ? x * (q + 1) : rm * (q + 1) + (x - rm) * q) + bid / 8;
   }
@@ -864,8 +876,24 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
     float v[W];
 #pragma unroll
     for (int i = 0; i < W; ++i) v[i] = 0.f;
-    for (int s = 0; s < p.splits; ++s) {
-      const float* src = p.ws + ((int64_t)s * nb + b) * per + mn;
+    const int64_t sstride = (int64_t)nb * per;
+    const float* src0 = p.ws + (int64_t)b * per + mn;
+    int s = 0;
+    if constexpr (V4) {
+      // four slab loads in flight per step, summed in split order (the same order, and so the
+      // same bits, as one at a time)
+      for (; s + 4 <= p.splits; s += 4) {
+        float4 t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t[u] = *(const float4*)(src0 + (s + u) * sstride);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[0] += t[u].x; v[1] += t[u].y; v[2] += t[u].z; v[3] += t[u].w;
+        }
+      }
+    }
+    for (; s < p.splits; ++s) {
+      const float* src = src0 + s * sstride;
       if constexpr (V4) {
         const float4 t = *(const float4*)src;
         v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
