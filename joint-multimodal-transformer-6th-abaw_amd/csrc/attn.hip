@@ -34,10 +34,13 @@
 //    LDS: K 64 KiB + V 64 KiB + exchange 32 KiB = 160 KiB.
 //  * Backward: 32-key tiles double-buffered (tile j+1's K and V land during tile j), scores and
 //    dP exchanged together.  LDS: 2 x (K 32 KiB + V 32 KiB) + exchange 32 KiB = 160 KiB.
-//  * Outputs (O, dQ) are staged through LDS and stored as whole 1-KiB rows.
+//  * Persistent grid (one block per CU, item_range): an item = (n, h, 64-row q-tile); the next
+//    item's row fragments and K / V tile 0 are issued during the current item's last tile, and
+//    the outputs (O, dQ) are stored straight from registers (16-B stores of paired accumulators),
+//    so consecutive items overlap their loads and stores (3-7 % over one block per item).
 //  * Waits: raw s_barrier after an explicit lgkmcnt(0); LDS-DMA retired by vmcnt before the
 //    barrier that precedes the read (never __syncthreads, whose fence would drain the DMA).
-//  * XCD-aware block order: the q-tile blocks of one (n, h) share K / V through one XCD's L2.
+//  * XCD-aware item order: the q-tiles of one (n, h) run on one XCD and share K / V in its L2.
 #include "common.h"
 
 namespace jmt {
@@ -55,11 +58,6 @@ constexpr int AB_LDS = 4 * AB_KT * AT_ROWB + 8 * AT_XCH;   // 160 KiB
 __device__ __forceinline__ int img_off(int row, int b) {
   return row * AT_ROWB + ((((b >> 4) ^ ((row & 7) << 1))) << 4) + (b & 15);
 }
-// output staging image (16-row swizzle: conflict-free ds_write_b64 of a 16-row fragment)
-__device__ __forceinline__ int out_off(int row, int b) {
-  return row * AT_ROWB + ((((b >> 4) ^ (row & 15))) << 4) + (b & 15);
-}
-
 // Per-lane base offsets of the fragment reads (the swizzle XOR touches chunk bits 1-3 only, so
 // a read's offset = one of a few lane bases + a compile-time immediate):
 //  row_base(m): ds_read_b128 fragment of row li (+16 kt), chunk 4 (4 a + m) + g of half h
@@ -110,30 +108,49 @@ __device__ __forceinline__ int xcd_block() {
   return wg;
 }
 
-// store this wave's 16 x 256 accumulator half (lane: row li, dims 256 h + 16 t + 4 g + r,
-// multiplied by `mul`) through the LDS staging image, then whole rows to global memory.
-// Every wave must have finished reading the LDS region before the call.
-template <typename T>
-__device__ __forceinline__ void store_rows(char* stage, const f32x4* acc, float mul, T* out,
-                                           int64_t so_l, int q0, int Lq) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int g = lane >> 4, li = lane & 15, rg = w & 3, h = w >> 2;
-  const int row = 16 * rg + li;
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    T v4[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v4[r] = from_f<T>(acc[t][r] * mul);
-    *(uint2*)(stage + out_off(row, (256 * h + 16 * t + 4 * g) * 2)) = *(const uint2*)v4;
+// Persistent work distribution over `nitems` (n, h, q-tile) items, item = (n H + h) nqt + qt.
+// A grid of one block per CU (a multiple of 8) deals the items to the 8 XCDs in contiguous
+// ranges; block b (XCD b % 8, slot b / 8) takes items lo + slot, lo + slot + G/8, ...  so at any
+// moment an XCD's blocks work on consecutive items and the q-tiles of one (n, h) share its K / V
+// through that XCD's L2.  A grid of one block per item keeps the xcd_block() order.
+__device__ __forceinline__ void item_range(int nitems, int& first, int& end, int& stride) {
+  const int G = gridDim.x;
+  if (G < nitems && G % 8 == 0) {
+    const int x = blockIdx.x % 8, S8 = G / 8;
+    first = (int)((int64_t)nitems * x / 8) + blockIdx.x / 8;
+    end = (int)((int64_t)nitems * (x + 1) / 8);
+    stride = S8;
+  } else {
+    first = G < nitems ? blockIdx.x : xcd_block();
+    end = nitems;
+    stride = G;
   }
-  lds_barrier();
+}
+
+// Store this wave's 16 x 256 accumulator half (lane: row li, dims 16 t + 4 g + r of `out`'s
+// half, multiplied by `mul`) straight from registers: the accumulators of sub-tiles t, t+1 are
+// paired with v_permlane16_swap so a lane holds 8 consecutive dims -> one 16-B store per lane and
+// pair (as gemm.hip's epilogue).  No LDS, no barrier: the next item's tiles may already be landing.
+template <typename T>
+__device__ __forceinline__ void store_acc_direct(const f32x4* acc, float mul, T* orow, bool valid) {
+  const int g = (threadIdx.x & 63) >> 4;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = 8 * w + i;
-    if (q0 + r < Lq) {
-      const uint4 v = *(const uint4*)(stage + out_off(r, lane * 16));
-      *(uint4*)(out + (int64_t)(q0 + r) * so_l + lane * 8) = v;
-    }
+  for (int jp = 0; jp < 8; ++jp) {
+    uint32_t pk[2][2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        T two[2] = {from_f<T>(acc[2 * jp + hh][2 * q] * mul),
+                    from_f<T>(acc[2 * jp + hh][2 * q + 1] * mul)};
+        pk[hh][q] = *(const uint32_t*)two;
+      }
+    const auto r0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+    const auto r1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+    const int c = 16 * (2 * jp + (g & 1)) + 8 * (g >> 1);
+    const u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
+    if (valid) __builtin_nontemporal_store(v, (u32x4*)(orow + c));
   }
 }
 
@@ -144,7 +161,7 @@ struct AttnFwdArgs {
   void* o;
   float* lse;
   int64_t sq_l, sq_n, sk_l, sk_n, sv_l, sv_n, so_l, so_n;
-  int Lq, Lk, H;
+  int Lq, Lk, H, nitems;
   float scale_log2;
   uint64_t* stamps;
 };
@@ -174,29 +191,27 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15, rg = w & 3, h = w >> 2;
   const int nqt = (p.Lq + AT_QT - 1) / AT_QT;
-  const int wg = xcd_block();
-  const int nh = wg / nqt;
-  const int n = nh / p.H, hd = nh % p.H;
-  const int q0 = (wg % nqt) * AT_QT;
+  const int nkt = (p.Lk + AF_KT - 1) / AF_KT;
+  int item, iend, istride;
+  item_range(p.nitems, item, iend, istride);
+  if (item >= iend) return;
+
+  // item -> (n, head, first query row)
+  int nh = item / nqt, n = nh / p.H, hd = nh % p.H, q0 = (item % nqt) * AT_QT;
   const T* kb = (const T*)p.k + (int64_t)n * p.sk_n + hd * AT_DH;
   const T* vb = (const T*)p.v + (int64_t)n * p.sv_n + hd * AT_DH;
-  const int nkt = (p.Lk + AF_KT - 1) / AF_KT;
 
-  const int qr = q0 + 16 * rg + li;
   F qf[8];
-  {
-    const T* qrow = (const T*)p.q + (int64_t)n * p.sq_n + hd * AT_DH +
-                    (int64_t)min(qr, p.Lq - 1) * p.sq_l + 256 * h + 8 * g;
+  auto load_q = [&](int n_, int hd_, int q0_) {
+    const T* qrow = (const T*)p.q + (int64_t)n_ * p.sq_n + hd_ * AT_DH +
+                    (int64_t)min(q0_ + 16 * rg + li, p.Lq - 1) * p.sq_l + 256 * h + 8 * g;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const F*)(qrow + 32 * ks);
-  }
+  };
+  load_q(n, hd, q0);
   stage_rows<T, AF_KT>(kimg, kb, p.sk_l, 0, p.Lk);
   stage_rows<T, AF_KT>(vimg, vb, p.sv_l, 0, p.Lk);
 
-  f32x4 o[16];
-#pragma unroll
-  for (int t = 0; t < 16; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
   f32x4* xmine = (f32x4*)(xch + w * AT_XCH) + lane;
   const f32x4* xpart = (const f32x4*)(xch + (w ^ 4) * AT_XCH) + lane;
   int kb4[4], tb8[8];
@@ -205,133 +220,160 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
 #pragma unroll
   for (int c = 0; c < 8; ++c) tb8[c] = tr_base(c, li, g, h);
 
-  wait_vmcnt<AF_KT / 8>();                        // Q and K tile 0 landed (V 0 in flight)
-  lds_barrier();
-  stamp<STAMP>(p.stamps, 255);
-  for (int j = 0; j < nkt; ++j) {
-    stamp<STAMP>(p.stamps, 8 * j);
-    // ---- partial scores over this wave's 256 dims: s[kt][r] = <row qr, key 64j+16kt+4g+r>
-    f32x4 s[4];
+  // Per item: Q (registers) and K / V tile 0 (LDS) were issued during the previous item's last
+  // tile (K tile 0 and Q right after its score phase freed the K image and Q registers, V tile 0
+  // after its P V phase), so an item's loads overlap the previous item's softmax, P V and output
+  // stores instead of opening every block with a cold load.
+  while (true) {
+    const int qr = q0 + 16 * rg + li;
+    const int nxt = item + istride;
+    const bool more = nxt < iend;
+    const int nh2 = nxt / nqt, n2 = nh2 / p.H, hd2 = nh2 % p.H, q02 = (nxt % nqt) * AT_QT;
+    const T* kb2 = (const T*)p.k + (int64_t)n2 * p.sk_n + hd2 * AT_DH;
+    const T* vb2 = (const T*)p.v + (int64_t)n2 * p.sv_n + hd2 * AT_DH;
+
+    f32x4 o[16];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    {   // k-step batches of 4 fragments (key subtiles 0..3), double-buffered: the reads of
-        // batch ks+1 are in flight while the 4 MFMAs of batch ks run (pinned by sched_barrier)
-      F fa[4], fb[4];
-      auto kbatch = [&](F* dst, int ks) {
+    for (int t = 0; t < 16; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY, l_run = 0.f;
+
+    wait_vmcnt<AF_KT / 8>();                        // Q and K tile 0 landed (V 0 in flight)
+    lds_barrier();
+    stamp<STAMP>(p.stamps, 255);
+    for (int j = 0; j < nkt; ++j) {
+      stamp<STAMP>(p.stamps, 8 * j);
+      // ---- partial scores over this wave's 256 dims: s[kt][r] = <row qr, key 64j+16kt+4g+r>
+      f32x4 s[4];
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-          dst[kt] = *(const F*)(kimg + kb4[ks & 3] + 256 * (ks >> 2) + 16384 * kt);
-      };
-      kbatch(fa, 0);
+      for (int kt = 0; kt < 4; ++kt) s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      {   // k-step batches of 4 fragments (key subtiles 0..3), double-buffered: the reads of
+          // batch ks+1 are in flight while the 4 MFMAs of batch ks run (pinned by sched_barrier)
+        F fa[4], fb[4];
+        auto kbatch = [&](F* dst, int ks) {
 #pragma unroll
-      for (int ks = 0; ks < 8; ks += 2) {
-        kbatch(fb, ks + 1);
-        __builtin_amdgcn_sched_barrier(0);
+          for (int kt = 0; kt < 4; ++kt)
+            dst[kt] = *(const F*)(kimg + kb4[ks & 3] + 256 * (ks >> 2) + 16384 * kt);
+        };
+        kbatch(fa, 0);
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt) s[kt] = mfma16(fa[kt], qf[ks], s[kt]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (ks + 2 < 8) kbatch(fa, ks + 2);
-        __builtin_amdgcn_sched_barrier(0);
+        for (int ks = 0; ks < 8; ks += 2) {
+          kbatch(fb, ks + 1);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt) s[kt] = mfma16(fb[kt], qf[ks + 1], s[kt]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    stamp<STAMP>(p.stamps, 8 * j + 1);
+          for (int kt = 0; kt < 4; ++kt) s[kt] = mfma16(fa[kt], qf[ks], s[kt]);
+          __builtin_amdgcn_sched_barrier(0);
+          if (ks + 2 < 8) kbatch(fa, ks + 2);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) xmine[64 * kt] = s[kt];
-    wait_vmcnt<0>();                              // V tile j landed
-    stamp<STAMP>(p.stamps, 8 * j + 2);
-    lds_barrier();                                // partials visible; K image free
-    stamp<STAMP>(p.stamps, 8 * j + 3);
-    if (j + 1 < nkt) stage_rows<T, AF_KT>(kimg, kb, p.sk_l, AF_KT * (j + 1), p.Lk);
-    const int kbase = AF_KT * j + 4 * g;
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      const f32x4 ps = xpart[64 * kt];
-      const f32x4 full = h == 0 ? s[kt] + ps : ps + s[kt];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float x = (kbase + 16 * kt + r < p.Lk) ? full[r] * p.scale_log2 : -INFINITY;
-        s[kt][r] = x;
-        mx = fmaxf(mx, x);
-      }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    if (__any(mx > m_run + 8.f)) {                // lazy rescale (header)
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      m_run = m_new;
-      l_run *= alpha;
-#pragma unroll
-      for (int t = 0; t < 16; ++t) o[t] *= alpha;
-    }
-    F pf[2];
-    float ls = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float pv = __builtin_amdgcn_exp2f(s[kt][r] - m_run);
-        ls += pv;
-        pf[kt >> 1][(kt & 1) * 4 + r] = from_f<T>(pv);
-      }
-    l_run += ls;
-    stamp<STAMP>(p.stamps, 8 * j + 4);
-    // ---- o[t] += sum_k P(k) V[k][256h + 16t + 4g + r]: transposed fragment reads of the V
-    // image in double-buffered batches of 4 fragments (q = 4b + i: t = q % 16, u = q / 16)
-    {
-      F fa[4], fb[4];
-      auto vbatch = [&](F* dst, int b) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int q = 4 * b + i, u = q >> 4, t = q & 15;
-          const char* a = vimg + tb8[t & 7] + 256 * (t >> 3) + 32768 * u;
-          const Hf lo = tr_read<Hf>(a);
-          const Hf hi = tr_read<Hf>(a + 16384);
-          dst[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          for (int kt = 0; kt < 4; ++kt) s[kt] = mfma16(fb[kt], qf[ks + 1], s[kt]);
+          __builtin_amdgcn_sched_barrier(0);
         }
-      };
-      vbatch(fa, 0);
+      }
+      stamp<STAMP>(p.stamps, 8 * j + 1);
 #pragma unroll
-      for (int b = 0; b < 8; b += 2) {
-        vbatch(fb, b + 1);
-        __builtin_amdgcn_sched_barrier(0);
+      for (int kt = 0; kt < 4; ++kt) xmine[64 * kt] = s[kt];
+      wait_vmcnt<0>();                              // V tile j landed
+      stamp<STAMP>(p.stamps, 8 * j + 2);
+      lds_barrier();                                // partials visible; K image free
+      stamp<STAMP>(p.stamps, 8 * j + 3);
+      if (j + 1 < nkt) {
+        stage_rows<T, AF_KT>(kimg, kb, p.sk_l, AF_KT * (j + 1), p.Lk);
+      } else if (more) {                            // next item: K tile 0, then its Q
+        stage_rows<T, AF_KT>(kimg, kb2, p.sk_l, 0, p.Lk);
+        load_q(n2, hd2, q02);
+      }
+      const int kbase = AF_KT * j + 4 * g;
+      float mx = -INFINITY;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int q = 4 * b + i;
-          o[q & 15] = mfma16(fa[i], pf[q >> 4], o[q & 15]);
+      for (int kt = 0; kt < 4; ++kt) {
+        const f32x4 ps = xpart[64 * kt];
+        const f32x4 full = h == 0 ? s[kt] + ps : ps + s[kt];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = (kbase + 16 * kt + r < p.Lk) ? full[r] * p.scale_log2 : -INFINITY;
+          s[kt][r] = x;
+          mx = fmaxf(mx, x);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        if (b + 2 < 8) vbatch(fa, b + 2);
-        __builtin_amdgcn_sched_barrier(0);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (__any(mx > m_run + 8.f)) {                // lazy rescale (header)
+        const float m_new = fmaxf(m_run, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        l_run *= alpha;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int q = 4 * (b + 1) + i;
-          o[q & 15] = mfma16(fb[i], pf[q >> 4], o[q & 15]);
+        for (int t = 0; t < 16; ++t) o[t] *= alpha;
+      }
+      F pf[2];
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(s[kt][r] - m_run);
+          ls += pv;
+          pf[kt >> 1][(kt & 1) * 4 + r] = from_f<T>(pv);
         }
-        __builtin_amdgcn_sched_barrier(0);
+      l_run += ls;
+      stamp<STAMP>(p.stamps, 8 * j + 4);
+      // ---- o[t] += sum_k P(k) V[k][256h + 16t + 4g + r]: transposed fragment reads of the V
+      // image in double-buffered batches of 4 fragments (q = 4b + i: t = q % 16, u = q / 16)
+      {
+        F fa[4], fb[4];
+        auto vbatch = [&](F* dst, int b) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int q = 4 * b + i, u = q >> 4, t = q & 15;
+            const char* a = vimg + tb8[t & 7] + 256 * (t >> 3) + 32768 * u;
+            const Hf lo = tr_read<Hf>(a);
+            const Hf hi = tr_read<Hf>(a + 16384);
+            dst[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+        };
+        vbatch(fa, 0);
+#pragma unroll
+        for (int b = 0; b < 8; b += 2) {
+          vbatch(fb, b + 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int q = 4 * b + i;
+            o[q & 15] = mfma16(fa[i], pf[q >> 4], o[q & 15]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (b + 2 < 8) vbatch(fa, b + 2);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int q = 4 * (b + 1) + i;
+            o[q & 15] = mfma16(fb[i], pf[q >> 4], o[q & 15]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      stamp<STAMP>(p.stamps, 8 * j + 5);
+      if (j + 1 < nkt) {
+        wait_vmcnt<0>();                            // K tile j+1 landed
+        stamp<STAMP>(p.stamps, 8 * j + 6);
+        lds_barrier();                              // V image and exchange slots free
+        stage_rows<T, AF_KT>(vimg, vb, p.sv_l, AF_KT * (j + 1), p.Lk);
       }
     }
-    stamp<STAMP>(p.stamps, 8 * j + 5);
-    if (j + 1 < nkt) {
-      wait_vmcnt<0>();                            // K tile j+1 landed
-      stamp<STAMP>(p.stamps, 8 * j + 6);
-      lds_barrier();                              // V image and exchange slots free
-      stage_rows<T, AF_KT>(vimg, vb, p.sv_l, AF_KT * (j + 1), p.Lk);
-    }
+    stamp<STAMP>(p.stamps, 254);
+    float lt = l_run;
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (qr < p.Lq && g == 0 && h == 0 && p.lse)
+      p.lse[(int64_t)nh * p.Lq + qr] = (m_run + __builtin_amdgcn_logf(lt)) * 0.69314718055994531f;
+    store_acc_direct<T>(o, 1.f / lt,
+                        (T*)p.o + (int64_t)n * p.so_n + hd * AT_DH + (int64_t)qr * p.so_l + 256 * h,
+                        qr < p.Lq);
+    if (!more) break;
+    lds_barrier();                                  // every wave is done with the V image
+    stage_rows<T, AF_KT>(vimg, vb2, p.sv_l, 0, p.Lk);
+    item = nxt; nh = nh2; n = n2; hd = hd2; q0 = q02; kb = kb2; vb = vb2;
   }
-  stamp<STAMP>(p.stamps, 254);
-  float lt = l_run;
-  lt += __shfl_xor(lt, 16, 64);
-  lt += __shfl_xor(lt, 32, 64);
-  if (qr < p.Lq && g == 0 && h == 0 && p.lse)
-    p.lse[(int64_t)nh * p.Lq + qr] = (m_run + __builtin_amdgcn_logf(lt)) * 0.69314718055994531f;
-  lds_barrier();                                  // every wave is done with the V image
-  store_rows<T>(kimg, o, 1.f / lt,
-                (T*)p.o + (int64_t)n * p.so_n + hd * AT_DH, p.so_l, q0, p.Lq);
 }
 
 
@@ -351,7 +393,7 @@ struct AttnBwdArgs {
   void* dsbuf;
   void* dq;
   int64_t sgo_l, sgo_n, so_l, so_n, sq_l, sq_n, sk_l, sk_n, sv_l, sv_n, sdq_l, sdq_n, ldp;
-  int Lq, Lk, H;
+  int Lq, Lk, H, nitems;
   float scale, scale_log2;
 };
 
@@ -366,171 +408,214 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15, rg = w & 3, h = w >> 2;
   const int nqt = (p.Lq + AT_QT - 1) / AT_QT;
-  const int wg = xcd_block();
-  const int nh = wg / nqt;
-  const int n = nh / p.H, hd = nh % p.H;
-  const int q0 = (wg % nqt) * AT_QT;
+  const int nkt = (p.Lk + AB_KT - 1) / AB_KT;
+  int item, iend, istride;
+  item_range(p.nitems, item, iend, istride);
+  if (item >= iend) return;
+
+  int nh = item / nqt, n = nh / p.H, hd = nh % p.H, q0 = (item % nqt) * AT_QT;
   const T* kb = (const T*)p.k + (int64_t)n * p.sk_n + hd * AT_DH;
   const T* vb = (const T*)p.v + (int64_t)n * p.sv_n + hd * AT_DH;
-  const int nkt = (p.Lk + AB_KT - 1) / AB_KT;
 
-  const int qr = q0 + 16 * rg + li;
-  const int qc = min(qr, p.Lq - 1);
-  const int64_t prow = (int64_t)nh * p.Lq + qc;
-  F qf[8], df[8];
-  float delta;
-  {
-    const int64_t coff = (int64_t)hd * AT_DH + 256 * h + 8 * g;
-    const T* qrow = (const T*)p.q + (int64_t)n * p.sq_n + (int64_t)qc * p.sq_l + coff;
-    const T* drow = (const T*)p.go + (int64_t)n * p.sgo_n + (int64_t)qc * p.sgo_l + coff;
-    const T* orow = (const T*)p.o + (int64_t)n * p.so_n + (int64_t)qc * p.so_l + coff;
-    float dp = 0.f;
+  // row-operand fragments of an item: Q, dO (kept for the whole item) and O (Delta only)
+  F qf[8], df[8], of[8];
+  auto rows_off = [&](int q0_) { return (int64_t)min(q0_ + 16 * rg + li, p.Lq - 1); };
+  auto load_qd = [&](int n_, int hd_, int q0_) {
+    const int64_t qc_ = rows_off(q0_), coff = (int64_t)hd_ * AT_DH + 256 * h + 8 * g;
+    const T* qrow = (const T*)p.q + (int64_t)n_ * p.sq_n + qc_ * p.sq_l + coff;
+    const T* drow = (const T*)p.go + (int64_t)n_ * p.sgo_n + qc_ * p.sgo_l + coff;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       qf[ks] = *(const F*)(qrow + 32 * ks);
       df[ks] = *(const F*)(drow + 32 * ks);
-      const F of = *(const F*)(orow + 32 * ks);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dp += (float)of[e] * (float)df[ks][e];
     }
-    dp += __shfl_xor(dp, 16, 64);
-    dp += __shfl_xor(dp, 32, 64);
-    delta = dp;                                   // this half's part of rowsum(dO o O)
-  }
-  const float lse2 = p.lse[prow] * 1.4426950408889634f;
+  };
+  auto load_o = [&](int n_, int hd_, int q0_) {
+    const int64_t qc_ = rows_off(q0_), coff = (int64_t)hd_ * AT_DH + 256 * h + 8 * g;
+    const T* orow = (const T*)p.o + (int64_t)n_ * p.so_n + qc_ * p.so_l + coff;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) of[ks] = *(const F*)(orow + 32 * ks);
+  };
+  load_qd(n, hd, q0);
+  load_o(n, hd, q0);
+  int buf = 0;                                    // buffer pair of the next tile to compute
   stage_rows<T, AB_KT>(smem, kb, p.sk_l, 0, p.Lk);
   stage_rows<T, AB_KT>(smem + IMG, vb, p.sv_l, 0, p.Lk);
-  ((float*)xch)[w * 64 + lane] = delta;
 
-  f32x4 acc[16];
-#pragma unroll
-  for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4* xmine = (f32x4*)(xch + w * AT_XCH) + lane;
   const f32x4* xpart = (const f32x4*)(xch + (w ^ 4) * AT_XCH) + lane;
-  T* prow_p = (T*)p.pbuf + prow * p.ldp;
-  T* prow_ds = (T*)p.dsbuf + prow * p.ldp;
   int kb4[4], tb8[8];
 #pragma unroll
   for (int m = 0; m < 4; ++m) kb4[m] = row_base(m, li, g, h);
 #pragma unroll
   for (int c = 0; c < 8; ++c) tb8[c] = tr_base(c, li, g, h);
 
-  wait_vmcnt<0>();                                // tile 0 landed
-  lds_barrier();                                  // ... and every Delta part written
-  {
-    const float part = ((const float*)xch)[(w ^ 4) * 64 + lane];
-    delta = h == 0 ? delta + part : part + delta;
-  }
-  lds_barrier();                                  // Delta parts read: exchange slots free
+  // Persistent items (item_range): the next item's Q / dO / O fragments are loaded right after
+  // the last tile's score phase (their registers are free from there on) and its K / V tile 0
+  // into the free buffer pair at the start of the last tile, so an item opens on landed data.
+  while (true) {
+    const int qr = q0 + 16 * rg + li;
+    const int qc = min(qr, p.Lq - 1);
+    const int64_t prow = (int64_t)nh * p.Lq + qc;
+    const int nxt = item + istride;
+    const bool more = nxt < iend;
+    const int nh2 = nxt / nqt, n2 = nh2 / p.H, hd2 = nh2 % p.H, q02 = (nxt % nqt) * AT_QT;
+    const T* kb2 = (const T*)p.k + (int64_t)n2 * p.sk_n + hd2 * AT_DH;
+    const T* vb2 = (const T*)p.v + (int64_t)n2 * p.sv_n + hd2 * AT_DH;
 
-  for (int j = 0; j < nkt; ++j) {
-    const char* kimg = smem + (j & 1) * 2 * IMG;
-    const char* vimg = kimg + IMG;
-    if (j + 1 < nkt) {                            // tile j+1 into the other buffer pair
-      char* nk = smem + ((j + 1) & 1) * 2 * IMG;
-      stage_rows<T, AB_KT>(nk, kb, p.sk_l, AB_KT * (j + 1), p.Lk);
-      stage_rows<T, AB_KT>(nk + IMG, vb, p.sv_l, AB_KT * (j + 1), p.Lk);
-    }
-    // ---- partial scores (K) and partial dP (V) over this wave's 256 dims
-    f32x4 s[2], d[2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      d[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    {   // k-step batches (K and V fragments of key subtiles 0, 1), double-buffered
-      F fa[4], fb[4];
-      auto batch = [&](F* dst, int ks) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          const int o = kb4[ks & 3] + 256 * (ks >> 2) + 16384 * kt;
-          dst[kt] = *(const F*)(kimg + o);
-          dst[2 + kt] = *(const F*)(vimg + o);
-        }
-      };
-      batch(fa, 0);
-#pragma unroll
-      for (int ks = 0; ks < 8; ks += 2) {
-        batch(fb, ks + 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          s[kt] = mfma16(fa[kt], qf[ks], s[kt]);
-          d[kt] = mfma16(fa[2 + kt], df[ks], d[kt]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (ks + 2 < 8) batch(fa, ks + 2);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          s[kt] = mfma16(fb[kt], qf[ks + 1], s[kt]);
-          d[kt] = mfma16(fb[2 + kt], df[ks + 1], d[kt]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    xmine[0] = s[0];
-    xmine[64] = s[1];
-    xmine[128] = d[0];
-    xmine[192] = d[1];
-    lds_barrier();                                // partials visible (tile j+1 DMA in flight)
-    const int kbase = AB_KT * j + 4 * g;
-    F dsf;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const f32x4 ps = xpart[64 * kt], pd = xpart[128 + 64 * kt];
-      const f32x4 sf = h == 0 ? s[kt] + ps : ps + s[kt];
-      const f32x4 dfull = h == 0 ? d[kt] + pd : pd + d[kt];
-      T pv4[4], ds4[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool in = kbase + 16 * kt + r < p.Lk;
-        const float pv = in ? __builtin_amdgcn_exp2f(sf[r] * p.scale_log2 - lse2) : 0.f;
-        const float ds = p.scale * pv * (dfull[r] - delta);
-        pv4[r] = from_f<T>(pv);
-        ds4[r] = from_f<T>(ds);
-        dsf[kt * 4 + r] = ds4[r];
-      }
-      const int key = kbase + 16 * kt;
-      if (qr < p.Lq && key < p.ldp) {
-        if (h == 0) *(uint2*)(prow_p + key) = *(const uint2*)pv4;
-        else *(uint2*)(prow_ds + key) = *(const uint2*)ds4;
-      }
-    }
-    // ---- acc[t] += sum_k dS(k) K[k][256h + 16t + 4g + r] (transposed K fragments in
-    // double-buffered batches of 4)
+    float delta;
     {
-      F fa[4], fb[4];
-      auto kbatch = [&](F* dst, int b) {
+      float dp = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int t = 4 * b + i;
-          const char* a = kimg + tb8[t & 7] + 256 * (t >> 3);
-          const Hf lo = tr_read<Hf>(a);
-          const Hf hi = tr_read<Hf>(a + 16384);
-          dst[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-      };
-      kbatch(fa, 0);
+      for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
-      for (int b = 0; b < 4; b += 2) {
-        kbatch(fb, b + 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[4 * b + i] = mfma16(fa[i], dsf, acc[4 * b + i]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (b + 2 < 4) kbatch(fa, b + 2);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[4 * b + 4 + i] = mfma16(fb[i], dsf, acc[4 * b + 4 + i]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+        for (int e = 0; e < 8; ++e) dp += (float)of[ks][e] * (float)df[ks][e];
+      dp += __shfl_xor(dp, 16, 64);
+      dp += __shfl_xor(dp, 32, 64);
+      delta = dp;                                   // this half's part of rowsum(dO o O)
     }
-    wait_vmcnt<0>();                              // tile j+1 landed (and P / dS stores issued)
-    lds_barrier();                                // this buffer pair and the slots are free
+    const float lse2 = p.lse[prow] * 1.4426950408889634f;
+    ((float*)xch)[w * 64 + lane] = delta;
+
+    f32x4 acc[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    T* prow_p = (T*)p.pbuf + prow * p.ldp;
+    T* prow_ds = (T*)p.dsbuf + prow * p.ldp;
+
+    wait_vmcnt<0>();                                // tile 0 landed
+    lds_barrier();                                  // ... and every Delta part written
+    {
+      const float part = ((const float*)xch)[(w ^ 4) * 64 + lane];
+      delta = h == 0 ? delta + part : part + delta;
+    }
+    lds_barrier();                                  // Delta parts read: exchange slots free
+
+    for (int j = 0; j < nkt; ++j) {
+      const char* kimg = smem + buf * 2 * IMG;
+      const char* vimg = kimg + IMG;
+      {
+        char* nk = smem + (buf ^ 1) * 2 * IMG;      // tile j+1 (or the next item's tile 0)
+        if (j + 1 < nkt) {
+          stage_rows<T, AB_KT>(nk, kb, p.sk_l, AB_KT * (j + 1), p.Lk);
+          stage_rows<T, AB_KT>(nk + IMG, vb, p.sv_l, AB_KT * (j + 1), p.Lk);
+        } else if (more) {
+          stage_rows<T, AB_KT>(nk, kb2, p.sk_l, 0, p.Lk);
+          stage_rows<T, AB_KT>(nk + IMG, vb2, p.sv_l, 0, p.Lk);
+        }
+      }
+      // ---- partial scores (K) and partial dP (V) over this wave's 256 dims
+      f32x4 s[2], d[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        d[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      {   // k-step batches (K and V fragments of key subtiles 0, 1), double-buffered
+        F fa[4], fb[4];
+        auto batch = [&](F* dst, int ks) {
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            const int o = kb4[ks & 3] + 256 * (ks >> 2) + 16384 * kt;
+            dst[kt] = *(const F*)(kimg + o);
+            dst[2 + kt] = *(const F*)(vimg + o);
+          }
+        };
+        batch(fa, 0);
+#pragma unroll
+        for (int ks = 0; ks < 8; ks += 2) {
+          batch(fb, ks + 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            s[kt] = mfma16(fa[kt], qf[ks], s[kt]);
+            d[kt] = mfma16(fa[2 + kt], df[ks], d[kt]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (ks + 2 < 8) batch(fa, ks + 2);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            s[kt] = mfma16(fb[kt], qf[ks + 1], s[kt]);
+            d[kt] = mfma16(fb[2 + kt], df[ks + 1], d[kt]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      xmine[0] = s[0];
+      xmine[64] = s[1];
+      xmine[128] = d[0];
+      xmine[192] = d[1];
+      lds_barrier();                                // partials visible (tile j+1 DMA in flight)
+      if (j + 1 == nkt && more) load_qd(n2, hd2, q02);     // next item's Q / dO fragments
+      const int kbase = AB_KT * j + 4 * g;
+      F dsf;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const f32x4 ps = xpart[64 * kt], pd = xpart[128 + 64 * kt];
+        const f32x4 sf = h == 0 ? s[kt] + ps : ps + s[kt];
+        const f32x4 dfull = h == 0 ? d[kt] + pd : pd + d[kt];
+        T pv4[4], ds4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool in = kbase + 16 * kt + r < p.Lk;
+          const float pv = in ? __builtin_amdgcn_exp2f(sf[r] * p.scale_log2 - lse2) : 0.f;
+          const float ds = p.scale * pv * (dfull[r] - delta);
+          pv4[r] = from_f<T>(pv);
+          ds4[r] = from_f<T>(ds);
+          dsf[kt * 4 + r] = ds4[r];
+        }
+        const int key = kbase + 16 * kt;
+        if (qr < p.Lq && key < p.ldp) {
+          if (h == 0) *(uint2*)(prow_p + key) = *(const uint2*)pv4;
+          else *(uint2*)(prow_ds + key) = *(const uint2*)ds4;
+        }
+      }
+      // ---- acc[t] += sum_k dS(k) K[k][256h + 16t + 4g + r] (transposed K fragments in
+      // double-buffered batches of 4)
+      {
+        F fa[4], fb[4];
+        auto kbatch = [&](F* dst, int b) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int t = 4 * b + i;
+            const char* a = kimg + tb8[t & 7] + 256 * (t >> 3);
+            const Hf lo = tr_read<Hf>(a);
+            const Hf hi = tr_read<Hf>(a + 16384);
+            dst[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+        };
+        kbatch(fa, 0);
+#pragma unroll
+        for (int b = 0; b < 4; b += 2) {
+          kbatch(fb, b + 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[4 * b + i] = mfma16(fa[i], dsf, acc[4 * b + i]);
+          __builtin_amdgcn_sched_barrier(0);
+          if (b + 2 < 4) kbatch(fa, b + 2);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[4 * b + 4 + i] = mfma16(fb[i], dsf, acc[4 * b + 4 + i]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (j + 1 < nkt) {
+        wait_vmcnt<0>();                            // tile j+1 landed (and P / dS stores issued)
+        lds_barrier();                              // this buffer pair and the slots are free
+      }
+      buf ^= 1;
+    }
+    store_acc_direct<T>(acc, 1.f,
+                        (T*)p.dq + (int64_t)n * p.sdq_n + hd * AT_DH + (int64_t)qr * p.sdq_l +
+                            256 * h,
+                        qr < p.Lq);
+    if (!more) break;
+    load_o(n2, hd2, q02);                           // O of the next item (Delta), after acc is dead
+    lds_barrier();                                  // every wave is done with the last tile's
+                                                    // images and exchange slots
+    item = nxt; nh = nh2; n = n2; hd = hd2; q0 = q02; kb = kb2; vb = vb2;
   }
-  store_rows<T>(smem, acc, 1.f, (T*)p.dq + (int64_t)n * p.sdq_n + hd * AT_DH, p.sdq_l, q0,
-                p.Lq);
 }
 
 template <typename K>
@@ -556,6 +641,22 @@ static int check_common(const char* name, int N, int H, int Lq, int Lk, const vo
 using namespace jmt;
 
 static void* g_stamps = nullptr;
+
+// one block per CU (the 160 KiB of LDS admit one), rounded down to a multiple of 8 (XCDs), when
+// there are more items than CUs; otherwise one block per item
+static unsigned persistent_grid(int nitems) {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 8)
+      v = 8;
+    ncu = v / 8 * 8;
+    const char* e = getenv("JMT_ATTN_PERSIST");   // dev A/B switch: 0 = one block per item
+    if (e && e[0] == '0') ncu = 1 << 30;
+  }
+  return (unsigned)(nitems > ncu ? ncu : nitems);
+}
 
 // diagnostic: route jmt_attn_fwd (bf16) through the phase-stamped kernel, stamps into `buf`
 // (2 x 256 x 64 uint64); NULL turns it off.  Not part of include/jmt.h (dev tool).
@@ -587,7 +688,8 @@ extern "C" int jmt_attn_fwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
   a.Lq = Lq; a.Lk = Lk; a.H = H;
   a.scale_log2 = scale * 1.4426950408889634f;
   hipStream_t st = as_stream(stream);
-  const dim3 grid((unsigned)(((Lq + AT_QT - 1) / AT_QT) * N * H));
+  a.nitems = ((Lq + AT_QT - 1) / AT_QT) * N * H;
+  const dim3 grid(persistent_grid(a.nitems));
   if (g_stamps && dt == JMT_BF16) {   // diagnostic: phase stamps (jmt_attn_set_stamps)
     a.stamps = (uint64_t*)g_stamps;
     static bool once = (set_lds(attn_fwd_kernel<__bf16, true>, AF_LDS), true);
@@ -632,7 +734,8 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
   a.Lq = Lq; a.Lk = Lk; a.H = H;
   a.scale = scale;
   a.scale_log2 = scale * 1.4426950408889634f;
-  const dim3 grid((unsigned)(((Lq + AT_QT - 1) / AT_QT) * N * H));
+  a.nitems = ((Lq + AT_QT - 1) / AT_QT) * N * H;
+  const dim3 grid(persistent_grid(a.nitems));
   hipStream_t st = as_stream(stream);
   if (dt == JMT_BF16) {
     static bool once = (set_lds(attn_bwd_kernel<__bf16>, AB_LDS), true);

@@ -365,7 +365,9 @@ def test_sgd_matches_torch_nesterov():
 
 @pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("Lq,Lk,N", [(300, 300, 3), (1, 6, 40), (6, 6, 17), (70, 129, 2),
-                                     (64, 64, 1), (129, 1, 2), (1024, 1024, 2)])
+                                     (64, 64, 1), (129, 1, 2), (1024, 1024, 2),
+                                     # more (n, q-tile) items than CUs: the persistent grid
+                                     (300, 300, 64), (70, 129, 200), (129, 1, 300)])
 def test_fused_attention_fwd_vs_fp32(cd, Lq, Lk, N):
     """jmt_attn_fwd (attn.hip) on packed self/cross-attention layouts vs softmax(QK^T/sqrt(d))V
     in fp32 from the same rounded inputs; the log-sum-exp against torch.logsumexp."""
@@ -397,7 +399,9 @@ def test_fused_attention_fwd_vs_fp32(cd, Lq, Lk, N):
 
 @pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("Lq,Lk,N", [(300, 300, 3), (1, 6, 40), (70, 129, 2), (129, 1, 2),
-                                     (1024, 1024, 1)])
+                                     (1024, 1024, 1),
+                                     # more (n, q-tile) items than CUs: the persistent grid
+                                     (300, 300, 64), (70, 129, 200), (129, 1, 300)])
 def test_fused_attention_bwd_vs_fp32(cd, Lq, Lk, N):
     """jmt_attn_bwd (attn.hip): P recomputed from the forward's lse, dS and dQ vs an fp32
     reference from the same rounded inputs (P and dS are stored in the compute dtype; the
