@@ -139,6 +139,7 @@ class GradBucketer:
         self.launch_log = []
 
     def begin(self):
+        self._main = torch.cuda.current_stream() if self.cuda else None
         self.left = dict(self.expected)
         self.bucket_left = [b[2] for b in self.buckets]
         self.launched = [False] * len(self.buckets)
@@ -171,6 +172,13 @@ class GradBucketer:
             ev = torch.cuda.Event()
             ev.record()                                   # after the bucket's last write
             self.comm.wait_event(ev)
+            # writes enqueued on the weight-gradient side stream (jmt.streams.run_side) and on
+            # the compute stream both precede the bucket's all-reduce
+            from . import streams
+            cur = torch.cuda.current_stream()
+            for st in streams.side_streams() + [self._main]:
+                if st is not None and st != cur and st.device == cur.device:
+                    self.comm.wait_stream(st)
             with torch.cuda.stream(self.comm):
                 self.works.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM,
                                                   group=self.group, async_op=True))

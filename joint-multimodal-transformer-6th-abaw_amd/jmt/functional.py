@@ -318,8 +318,12 @@ class LinearFn(Function):
                 if need[i]:
                     dxs[i] = outs[i] if in_dtypes[i] == cd else _cast_keep_layout(outs[i],
                                                                                   in_dtypes[i])
-        _wgrad(Gy, n, xin, L0.ld, kseg, W, r0, cd)
-        _bgrad(Gy, n, b, r0)
+
+        def param_grads():      # side stream (jmt.streams.run_side)
+            _wgrad(Gy, n, xin, L0.ld, kseg, W, r0, cd)
+            _bgrad(Gy, n, b, r0)
+
+        streams.run_side(param_grads, reads=(Gy.t,) + tuple(xin))
         return (None, None, None, None, None, *dxs)
 
 
@@ -363,20 +367,25 @@ class MLPFn(Function):
         dh = L.like(hid, cd)
         ldh = _ld(dh, L.perm)
         _dgrad(Gy, nout, W2, 0, cd, [dh], ldh, 1, hid, aux=h, ldaux=H.ld)
-        if odt == torch.float32 and cd != torch.float32 and nout <= 16:
-            # fp32 output (the V/A regressors' last layer, two_transformers.py:104-114): its
-            # weight / bias gradients are sums over all rows of the fp32 loss gradient, which
-            # nearly cancel (sum_i dL/dx_i = n c0 for the CCC): summing a 16-bit rounded copy
-            # would cost up to ~20 % relative error, so they are reduced from fp32 dY and an fp32
-            # copy of the (small) hidden activations with the exact-f32 MFMA GEMM.
-            G32 = _match(gy, Rows(L.like(nout, torch.float32)), torch.float32)
-            h32 = _cast_keep_layout(h, torch.float32)
-            H32 = Rows(h32)
-            _wgrad(G32, nout, [H32.t], H32.ld, hid, W2, 0, torch.float32)
-            _bgrad(G32, nout, b2, 0)
-        else:
-            _wgrad(Gy, nout, [h], H.ld, hid, W2, 0, cd)
-            _bgrad(Gy, nout, b2, 0)
+
+        def w2_grads():         # side stream (jmt.streams.run_side)
+            if odt == torch.float32 and cd != torch.float32 and nout <= 16:
+                # fp32 output (the V/A regressors' last layer, two_transformers.py:104-114): its
+                # weight / bias gradients are sums over all rows of the fp32 loss gradient,
+                # which nearly cancel (sum_i dL/dx_i = n c0 for the CCC): summing a 16-bit
+                # rounded copy would cost up to ~20 % relative error, so they are reduced from
+                # fp32 dY and an fp32 copy of the (small) hidden activations with the exact-f32
+                # MFMA GEMM.
+                G32 = _match(gy, Rows(L.like(nout, torch.float32)), torch.float32)
+                h32 = _cast_keep_layout(h, torch.float32)
+                H32 = Rows(h32)
+                _wgrad(G32, nout, [H32.t], H32.ld, hid, W2, 0, torch.float32)
+                _bgrad(G32, nout, b2, 0)
+            else:
+                _wgrad(Gy, nout, [h], H.ld, hid, W2, 0, cd)
+                _bgrad(Gy, nout, b2, 0)
+
+        streams.run_side(w2_grads, reads=(gy, Gy.t, h))
         Gh = Rows(dh)
         dx = None
         if ctx.needs_input_grad[5]:
@@ -384,8 +393,12 @@ class MLPFn(Function):
             _dgrad(Gh, hid, W1, 0, cd, [dx], _ld(dx, L.perm), 1, L.F)
             if xdt != cd:
                 dx = _cast_keep_layout(dx, xdt)
-        _wgrad(Gh, hid, [xin], L.ld, L.F, W1, 0, cd)
-        _bgrad(Gh, hid, b1, 0)
+
+        def w1_grads():
+            _wgrad(Gh, hid, [xin], L.ld, L.F, W1, 0, cd)
+            _bgrad(Gh, hid, b1, 0)
+
+        streams.run_side(w1_grads, reads=(dh, xin))
         return None, None, None, None, None, dx
 
 

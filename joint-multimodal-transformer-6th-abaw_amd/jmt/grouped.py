@@ -28,7 +28,7 @@ from typing import List, Sequence
 import torch
 from torch.autograd import Function
 
-from . import ops
+from . import ops, streams
 from .functional import (_dc, _grad_buffer, _grad_done, _ptr, attn_backward, attn_forward,
                          compute_dtype, weight_as)
 
@@ -406,6 +406,8 @@ class EncoderGroupFn(Function):
         dF1 = torch.empty(G, B, T, hid, dtype=cd, device=dev)
         _gemm_dgrad(dS.data_ptr(), E, R * E, R, E, [p[6] for p in P], 0, dF1.data_ptr(), hid,
                     R * hid, cdt, cd, dev, aux=F1, ldaux=hid)
+        # (W2's weight gradient stays on the compute stream: on the side stream the in-place
+        # dH1 below would have to wait for it, which measured slower, profiles/r02_side_stream.txt)
         _gemm_wgrad([dS.data_ptr()], E, R * E, [F1.data_ptr()], hid, R * hid, R, E,
                     [p[6] for p in P], 0, cd, dev)
         if not b2_done:
@@ -413,10 +415,14 @@ class EncoderGroupFn(Function):
         # dH1 = dS2 + dF1 . W1  (in place on dS: beta = 1)
         _gemm_dgrad(dF1.data_ptr(), hid, R * hid, R, hid, [p[4] for p in P], 0, dS.data_ptr(),
                     E, R * E, cdt, cd, dev, beta=1.0)
-        _gemm_wgrad([dF1.data_ptr()], hid, R * hid, [H1.data_ptr()], E, R * E, R, hid,
-                    [p[4] for p in P], 0, cd, dev)
-        _bias_grad_grouped(dF1.data_ptr(), G, hid, R * hid, R, hid, [p[5] for p in P], 0, cd,
-                           dev)
+
+        def w1_grads():         # side stream: dF1 and H1 are not written again
+            _gemm_wgrad([dF1.data_ptr()], hid, R * hid, [H1.data_ptr()], E, R * E, R, hid,
+                        [p[4] for p in P], 0, cd, dev)
+            _bias_grad_grouped(dF1.data_ptr(), G, hid, R * hid, R, hid, [p[5] for p in P], 0,
+                               cd, dev)
+
+        streams.run_side(w1_grads, reads=(dF1, H1))
         # LN1: dS1 = d(X + A1)
         dS1 = torch.empty_like(dS)
         bo_done = ln_bwd(X, A1, dS, st1, [p[8] for p in P], [p[9] for p in P], dS1,
@@ -425,21 +431,31 @@ class EncoderGroupFn(Function):
         dO = dS     # reuse: dS is dead
         _gemm_dgrad(dS1.data_ptr(), E, R * E, R, E, [p[2] for p in P], 0, dO.data_ptr(), E,
                     R * E, cdt, cd, dev)
-        _gemm_wgrad([dS1.data_ptr()], E, R * E, [O.data_ptr()], E, R * E, R, E,
-                    [p[2] for p in P], 0, cd, dev)
-        if not bo_done:
-            _bias_grad_grouped(dS1.data_ptr(), G, E, R * E, R, E, [p[3] for p in P], 0, cd, dev)
+
+        def out_proj_grads():   # side stream, under the attention backward
+            _gemm_wgrad([dS1.data_ptr()], E, R * E, [O.data_ptr()], E, R * E, R, E,
+                        [p[2] for p in P], 0, cd, dev)
+            if not bo_done:
+                _bias_grad_grouped(dS1.data_ptr(), G, E, R * E, R, E, [p[3] for p in P], 0, cd,
+                                   dev)
+
+        streams.run_side(out_proj_grads, reads=(dS1, O))
         # attention core -> packed dQKV
         dQKV = torch.empty(G, B, T, 3 * E, dtype=cd, device=dev)
         dsf = dQKV.view(G * B, T, 3 * E).permute(1, 0, 2)
         attn_backward(asaved, dO.view(G * B, T, E).permute(1, 0, 2), dsf, dsf, dsf)
-        # in_proj: dX = dS1 + dQKV . W_in  (in place on dS1)
+        # in_proj: dX = dS1 + dQKV . W_in  (in place on dS1, once the side stream has read it)
+        streams.wait_side()
         _gemm_dgrad(dQKV.data_ptr(), 3 * E, R * 3 * E, R, 3 * E, [p[0] for p in P], 0,
                     dS1.data_ptr(), E, R * E, cdt, cd, dev, beta=1.0)
-        _gemm_wgrad([dQKV.data_ptr()], 3 * E, R * 3 * E, [X.data_ptr()], E, R * E, R, 3 * E,
-                    [p[0] for p in P], 0, cd, dev)
-        _bias_grad_grouped(dQKV.data_ptr(), G, 3 * E, R * 3 * E, R, 3 * E, [p[1] for p in P], 0,
-                           cd, dev)
+
+        def in_proj_grads():    # side stream: dQKV and X are not written again
+            _gemm_wgrad([dQKV.data_ptr()], 3 * E, R * 3 * E, [X.data_ptr()], E, R * E, R, 3 * E,
+                        [p[0] for p in P], 0, cd, dev)
+            _bias_grad_grouped(dQKV.data_ptr(), G, 3 * E, R * 3 * E, R, 3 * E,
+                               [p[1] for p in P], 0, cd, dev)
+
+        streams.run_side(in_proj_grads, reads=(dQKV, X))
         ctx.state = None
         return (dS1, None) + (None,) * len(params)
 
@@ -511,39 +527,50 @@ class CrossAttention6Fn(Function):
                 seen.append(set())
             halves[-1].append(i)
             seen[-1].add(m)
-        # out_proj
+        # out_proj: input gradient on the compute stream, weight / bias gradients on the side
+        # stream (jmt.streams.run_side) overlapping the attention backward
         dO = torch.empty(NP, B, T, E, dtype=cd, device=dev)
         _gemm_dgrad(dO6.data_ptr(), E, R * E, R, E, [M[m][2] for m, _, _ in pairs], 0,
                     dO.data_ptr(), E, R * E, cdt, cd, dev)
-        for h in halves:
-            _gemm_wgrad([_ptr(dO6, i * R * E) for i in h], E, 0, [O[i * B].data_ptr() for i in h],
-                        E, 0, R, E, [M[pairs[i][0]][2] for i in h], 0, cd, dev)
-        for h in halves:
-            if _consecutive(h):
-                _bias_grad_grouped(_ptr(dO6, h[0] * R * E), len(h), E, R * E, R, E,
-                                   [M[pairs[i][0]][3] for i in h], 0, cd, dev)
-            else:
-                for i in h:
-                    _bias_grad(dO6[i], E, R, E, M[pairs[i][0]][3], 0)
+
+        def out_proj_grads():
+            for h in halves:
+                _gemm_wgrad([_ptr(dO6, i * R * E) for i in h], E, 0,
+                            [O[i * B].data_ptr() for i in h], E, 0, R, E,
+                            [M[pairs[i][0]][2] for i in h], 0, cd, dev)
+            for h in halves:
+                if _consecutive(h):
+                    _bias_grad_grouped(_ptr(dO6, h[0] * R * E), len(h), E, R * E, R, E,
+                                       [M[pairs[i][0]][3] for i in h], 0, cd, dev)
+                else:
+                    for i in h:
+                        _bias_grad(dO6[i], E, R, E, M[pairs[i][0]][3], 0)
+
+        streams.run_side(out_proj_grads, reads=(dO6, O))
         # attention core -> packed dQKV (NP, B, T, 3E)
         dQKV = torch.empty(NP, B, T, 3 * E, dtype=cd, device=dev)
         dsf = dQKV.view(NP * B, T, 3 * E).permute(1, 0, 2)
         attn_backward(asaved, dO.view(NP * B, T, E).permute(1, 0, 2), dsf, dsf, dsf)
-        # in_proj weight gradients: query rows [0, E) from the query stream, key/value rows
-        # [E, 3E) from the key stream
-        for h in halves:
-            ws = [M[pairs[i][0]][0] for i in h]
-            _gemm_wgrad([_ptr(dQKV, i * R * 3 * E) for i in h], 3 * E, 0,
-                        [Y[pairs[i][1]].data_ptr() for i in h], E, 0, R, E, ws, 0, cd, dev)
-            _gemm_wgrad([_ptr(dQKV, i * R * 3 * E + E) for i in h], 3 * E, 0,
-                        [Y[pairs[i][2]].data_ptr() for i in h], E, 0, R, 2 * E, ws, E, cd, dev)
-        for h in halves:
-            if _consecutive(h):
-                _bias_grad_grouped(_ptr(dQKV, h[0] * R * 3 * E), len(h), 3 * E, R * 3 * E, R,
-                                   3 * E, [M[pairs[i][0]][1] for i in h], 0, cd, dev)
-            else:
-                for i in h:
-                    _bias_grad(dQKV[i], 3 * E, R, 3 * E, M[pairs[i][0]][1], 0)
+
+        # in_proj weight gradients (side stream, overlapping the stream dgrads): query rows
+        # [0, E) from the query stream, key/value rows [E, 3E) from the key stream
+        def in_proj_grads():
+            for h in halves:
+                ws = [M[pairs[i][0]][0] for i in h]
+                _gemm_wgrad([_ptr(dQKV, i * R * 3 * E) for i in h], 3 * E, 0,
+                            [Y[pairs[i][1]].data_ptr() for i in h], E, 0, R, E, ws, 0, cd, dev)
+                _gemm_wgrad([_ptr(dQKV, i * R * 3 * E + E) for i in h], 3 * E, 0,
+                            [Y[pairs[i][2]].data_ptr() for i in h], E, 0, R, 2 * E, ws, E, cd,
+                            dev)
+            for h in halves:
+                if _consecutive(h):
+                    _bias_grad_grouped(_ptr(dQKV, h[0] * R * 3 * E), len(h), 3 * E, R * 3 * E,
+                                       R, 3 * E, [M[pairs[i][0]][1] for i in h], 0, cd, dev)
+                else:
+                    for i in h:
+                        _bias_grad(dQKV[i], 3 * E, R, 3 * E, M[pairs[i][0]][1], 0)
+
+        streams.run_side(in_proj_grads, reads=(dQKV, Y))
         # stream gradients: every use of stream s (as a query: rows [0,E) of W_in; as a key /
         # value: rows [E,2E) and [2E,3E)) is one K-segment of ONE dgrad GEMM (K = nseg * E)
         dY = torch.zeros(S, B, T, E, dtype=cd, device=dev) if any(
@@ -620,15 +647,20 @@ class ConcatLinearFn(Function):
                  a=[dy.data_ptr()], lda=N, a_kmajor=True, sA=(0, 0),
                  b=[Wc.data_ptr()], ldb=S * E, b_kmajor=False, sB=(E, 0),
                  c=[dX.data_ptr()], ldc=E, sC=(R * E, 0), batch0=S, device=dev)
-        gW = _grad_buffer(W)
-        if gW is not None:
-            ops.gemm(M=N, N=E, K=R, ab_dtype=_dc(cd), c_dtype=ops.F32,
-                     a=[dy.data_ptr()], lda=N, a_kmajor=False, sA=(0, 0),
-                     b=[X.data_ptr()], ldb=E, b_kmajor=False, sB=(R * E, 0),
-                     c=[gW.data_ptr()], ldc=S * E, sC=(E, 0), batch0=S, beta=1.0, device=dev)
-            _grad_done(W)
-        if b is not None:
-            _bias_grad(dy, N, R, N, b, 0)
+
+        def param_grads():      # side stream: overlaps the dgrads of the cross-attentions
+            gW = _grad_buffer(W)
+            if gW is not None:
+                ops.gemm(M=N, N=E, K=R, ab_dtype=_dc(cd), c_dtype=ops.F32,
+                         a=[dy.data_ptr()], lda=N, a_kmajor=False, sA=(0, 0),
+                         b=[X.data_ptr()], ldb=E, b_kmajor=False, sB=(R * E, 0),
+                         c=[gW.data_ptr()], ldc=S * E, sC=(E, 0), batch0=S, beta=1.0,
+                         device=dev)
+                _grad_done(W)
+            if b is not None:
+                _bias_grad(dy, N, R, N, b, 0)
+
+        streams.run_side(param_grads, reads=(dy, X))
         return dX, None, None
 
 

@@ -9,12 +9,13 @@ forward node, so the backward overlaps the same way."""
 from __future__ import annotations
 
 import os
-from typing import Callable, List, Sequence
+from typing import Callable, List, Optional, Sequence
 
 import torch
 
 _pool: dict = {}
-_enabled = {"on": True, "capture": os.environ.get("JMT_CAPTURE_STREAMS", "1") != "0"}
+_enabled = {"on": True, "capture": os.environ.get("JMT_CAPTURE_STREAMS", "1") != "0",
+            "side": os.environ.get("JMT_SIDE_STREAM", "1") != "0"}
 
 
 def set_enabled(on: bool) -> None:
@@ -90,3 +91,66 @@ def run_parallel(fns: Sequence[Callable[[], object]], device) -> list:
     for o in outs:
         mark(o)
     return outs
+
+
+# ------------------------------------------------------------------ weight-gradient side stream
+# In a backward pass the input-gradient (dgrad) GEMMs form the critical chain; the weight- and
+# bias-gradient launches of a layer only read that layer's output gradient and saved input and
+# write parameter gradients.  They go to one side stream per device, forked from the compute
+# stream right after the output gradient is enqueued, so their blocks fill the CUs the chain's
+# launches leave idle (tile-quantised last rounds, epilogue bursts, latency-bound phases).
+_side: dict = {}
+_side_join = {"queued": False}
+
+
+def set_side_enabled(on: bool) -> None:
+    _enabled["side"] = bool(on)
+
+
+def side_streams() -> List[torch.cuda.Stream]:
+    """The side streams created so far (jmt.dist.GradBucketer gates its all-reduces on them)."""
+    return list(_side.values())
+
+
+def run_side(fn: Callable[[], object], reads: Sequence[Optional[torch.Tensor]] = ()):
+    """Enqueue fn() on the current device's side stream after everything already queued on the
+    current stream.  `reads`: tensors fn's kernels read that the caller may drop before they run
+    (marked used on the side stream for the caching allocator).  Parameter-gradient writes of
+    different streams must not target the same memory: callers move ALL writes of a gradient
+    buffer to the side stream.  The caller's stream joins the side stream at the end of the
+    backward pass (a queued autograd callback), before the optimizer reads the gradients."""
+    if not (_enabled["on"] and _enabled["side"]) or \
+            (torch.cuda.is_current_stream_capturing() and not _enabled["capture"]):
+        return fn()
+    main = torch.cuda.current_stream()
+    dev = main.device.index if main.device.index is not None else torch.cuda.current_device()
+    side = _side.get(dev)
+    if side is None:
+        side = _side[dev] = torch.cuda.Stream(device=main.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        out = fn()
+    for t in reads:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            t.record_stream(side)
+    if not _side_join["queued"]:
+        _side_join["queued"] = True
+
+        def _cb():
+            _side_join["queued"] = False
+            cur = torch.cuda.current_stream()
+            for st in _side.values():
+                if st.device == cur.device:
+                    cur.wait_stream(st)
+
+        torch.autograd.Variable._execution_engine.queue_callback(_cb)
+    return out
+
+
+def wait_side() -> None:
+    """Make the current stream wait for the work queued so far on its device's side stream (a
+    kernel about to overwrite a buffer that side-stream work still reads)."""
+    cur = torch.cuda.current_stream()
+    for st in _side.values():
+        if st.device == cur.device:
+            cur.wait_stream(st)
