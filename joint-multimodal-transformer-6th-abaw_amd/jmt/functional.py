@@ -671,7 +671,8 @@ def attn_backward(saved, go, dq, dk, dv):
              b=[_ptr(q_src, qcol)], ldb=sq_l, b_kmajor=False, sB=(sq_n, dh),
              c=[_ptr(dk, kcol)], ldc=dk.stride(0), sC=(dk.stride(1), dh), batch0=N,
              batch1=H, device=dev)
-    # dV = P^T dO
+    # dV = P^T dO  (on the side stream, concurrent with dK, measured slower: the join waits
+    # for the weight gradients queued there before it; profiles/r02_side_stream.txt)
     ops.gemm(M=Lk, N=dh, K=Lq, ab_dtype=_dc(cd), c_dtype=_dc(cd),
              a=[P.data_ptr()], lda=ldS, a_kmajor=False, sA=bS,
              b=[go.data_ptr()], ldb=so_l, b_kmajor=False, sB=(so_n, dh),

@@ -154,3 +154,25 @@ def wait_side() -> None:
     for st in _side.values():
         if st.device == cur.device:
             cur.wait_stream(st)
+
+
+def fork_side(fn: Callable[[], object], reads: Sequence[Optional[torch.Tensor]] = ()) -> bool:
+    """Enqueue fn() on the side stream after the current stream's queued work, for the caller
+    to overlap with its next launch and then join with wait_side().  Returns False (fn ran on
+    the current stream) when side streams are off."""
+    if not (_enabled["on"] and _enabled["side"]) or \
+            (torch.cuda.is_current_stream_capturing() and not _enabled["capture"]):
+        fn()
+        return False
+    main = torch.cuda.current_stream()
+    dev = main.device.index if main.device.index is not None else torch.cuda.current_device()
+    side = _side.get(dev)
+    if side is None:
+        side = _side[dev] = torch.cuda.Stream(device=main.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        fn()
+    for t in reads:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            t.record_stream(side)
+    return True

@@ -2,10 +2,10 @@
 # weight-gradient side stream: all GPU tests, bench A/B (side stream off / on)
 set -u
 OUT=gpurun_out; mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/s3f_tests.log 2>&1
-rc=$?; echo "tests exit $rc"; tail -3 $OUT/s3f_tests.log
-if [ $rc -gt 1 ]; then grep -E "FAIL|Error" $OUT/s3f_tests.log | head; exit $rc; fi
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/s3h_tests.log 2>&1
+rc=$?; echo "tests exit $rc"; tail -3 $OUT/s3h_tests.log
+if [ $rc -gt 1 ]; then grep -E "FAIL|Error" $OUT/s3h_tests.log | head; exit $rc; fi
 for m in 0 1 0 1; do
-  JMT_SIDE_STREAM=$m timeout -k 10 300 python bench.py --steps 100 --warmup 5 --no-cpu-baseline --no-parity --probe-steps 1 > $OUT/s3f_bench_$m.log 2>&1 || exit 1
-  echo "side=$m $(grep -o '"ms_per_step": [0-9.]*' $OUT/s3f_bench_$m.log | head -1)"
+  JMT_SIDE_STREAM=$m timeout -k 10 300 python bench.py --steps 100 --warmup 5 --no-cpu-baseline --no-parity --probe-steps 1 > $OUT/s3h_bench_$m.log 2>&1 || exit 1
+  echo "side=$m $(grep -o '"ms_per_step": [0-9.]*' $OUT/s3h_bench_$m.log | head -1)"
 done
