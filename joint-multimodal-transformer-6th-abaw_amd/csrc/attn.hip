@@ -377,6 +377,10 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
 }
 
 
+// (A software-pipelined form — each tile's P V deferred into the next tile's iteration and
+// interleaved with its exponentials, the last P V of an item run in the next item's first
+// iteration — measured 3-8 % slower than this kernel at N = 96-384: profiles/
+// r02_attn_pipelined_fwd.txt.)
 // (A 4-wave, one-wave-per-SIMD forward with v_mfma_f32_32x32x16, 32 rows x all 512 dims per wave
 // and 128 rows per block — half the K/V bytes into LDS and half the LDS fragment bytes per FLOP —
 // needs ~480 registers per wave (O 256 + Q 128 + working set) and spilled 256 VGPRs under hipcc:
