@@ -328,6 +328,7 @@ def main():
     from jmt import functional as JF
     from jmt import ops
     from jmt import dist as jdist
+    from jmt import streams
     from jmt.optim import FusedSGD, GradScaler
     from jmt.graph import GraphedStep
     from models.two_transformers import Two_transformers
@@ -454,13 +455,18 @@ def main():
     if not args.no_probe:
         # per-launch HIP events cannot sit inside the replayed graph (and would add host work to
         # an eager timed region): the dominant kernel is timed over `probe_steps` eager steps
-        # right after the timed region, on the stream its launches go to
+        # right after the timed region, on the stream its launches go to.  The weight-gradient
+        # side stream (jmt.streams.run_side) is off for them: every launch then runs alone on the
+        # compute stream, so its event pair times the kernel itself, not the kernel plus the
+        # other stream's kernels sharing the CUs (profiles/r02_bench_family_check_s3.txt)
         ops.set_launch_hook(probe)
+        streams.set_side_enabled(False)
         probe.on = True
         for _ in range(args.probe_steps):
             step()
         torch.cuda.synchronize()
         probe.on = False
+        streams.set_side_enabled(os.environ.get("JMT_SIDE_STREAM", "1") != "0")
         ops.set_launch_hook(None)
     if world > 1:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -491,7 +497,8 @@ def main():
                     "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"] or None,
                     "avg_launch_us": dom["avg_launch_us"],
                     "launches_per_step": dom["launches_per_step"],
-                    "timed_over": f"{args.probe_steps} eager probe steps after the timed region, "
+                    "timed_over": f"{args.probe_steps} eager probe steps after the timed region "
+                                  "(side stream off: each launch alone on the compute stream), "
                                   "one event pair per launch minus the empty-launch pair "
                                   f"overhead ({psum['event_pair_overhead_us']} us)",
                     "families": psum["families"]}

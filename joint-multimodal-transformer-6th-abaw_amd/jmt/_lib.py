@@ -134,8 +134,9 @@ def load(path: str = LIB_PATH):
     if lib.jmt_abi_version() != 3:
         raise JMTError("libjmt_hip.so ABI version mismatch")
     cfg = int(os.environ.get("JMT_GEMM_CFG", "0"))   # development: force a GEMM pipeline config
-    if cfg:
-        lib.jmt_gemm_set_debug(cfg << 8)
+    dbg = int(os.environ.get("JMT_GEMM_DBG", "0"))   # development: gemm.hip ablation flags
+    if cfg or dbg:
+        lib.jmt_gemm_set_debug((cfg << 8) | (dbg & 0xff))
     _lib = lib
     return lib
 
