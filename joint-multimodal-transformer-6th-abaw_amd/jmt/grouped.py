@@ -33,6 +33,9 @@ from .functional import (_dc, _grad_buffer, _grad_done, _ptr, attn_backward, att
                          compute_dtype, weight_as)
 
 _enabled = {"on": os.environ.get("JMT_GROUPED", "1") != "0"}
+# the cross-attention backward's three stream-gradient GEMMs on branch streams: measured
+# 1.6 % slower per step (profiles/r02_par_stream_dgrad.txt), off unless JMT_PAR_STREAM_DGRAD=1
+_PAR_STREAM_DGRAD = os.environ.get("JMT_PAR_STREAM_DGRAD", "0") == "1"
 
 # the six cross-attentions in the reference's order (mm_multi_transformers.py:142-167), which is
 # also the order of torch.cat in the FC head (:201-211): (module, query stream, key/value stream)
@@ -577,6 +580,7 @@ class CrossAttention6Fn(Function):
             not any(q == s or k == s for _, q, k in pairs) for s in range(S)) else \
             torch.empty(S, B, T, E, dtype=cd, device=dev)
         keep = []     # the 16-bit weight copies must outlive the launches that read them
+        launches = []
         for s in range(S):
             a_ptrs, b_ptrs = [], []
             for i, (m, q, k) in enumerate(pairs):
@@ -588,12 +592,22 @@ class CrossAttention6Fn(Function):
                 if k == s:
                     a_ptrs += [_ptr(dQKV, i * R * 3 * E + E), _ptr(dQKV, i * R * 3 * E + 2 * E)]
                     b_ptrs += [_ptr(Wc, E * E), _ptr(Wc, 2 * E * E)]
-            for c0 in range(0, len(a_ptrs), 8):   # at most 8 K-segments per launch
-                ap, bp = a_ptrs[c0:c0 + 8], b_ptrs[c0:c0 + 8]
-                ops.gemm(M=R, N=E, K=len(ap) * E, ab_dtype=cdt, c_dtype=cdt,
-                         a=ap, lda=3 * E, a_kmajor=True, a_mode=2, a_kseg=E,
-                         b=bp, ldb=E, b_kmajor=False, b_mode=2, b_kseg=E,
-                         c=[dY[s].data_ptr()], ldc=E, beta=1.0 if c0 else 0.0, device=dev)
+            def stream_dgrad(a_ptrs=a_ptrs, b_ptrs=b_ptrs, c_ptr=dY[s].data_ptr()):
+                for c0 in range(0, len(a_ptrs), 8):   # at most 8 K-segments per launch
+                    ap, bp = a_ptrs[c0:c0 + 8], b_ptrs[c0:c0 + 8]
+                    ops.gemm(M=R, N=E, K=len(ap) * E, ab_dtype=cdt, c_dtype=cdt,
+                             a=ap, lda=3 * E, a_kmajor=True, a_mode=2, a_kseg=E,
+                             b=bp, ldb=E, b_kmajor=False, b_mode=2, b_kseg=E,
+                             c=[c_ptr], ldc=E, beta=1.0 if c0 else 0.0, device=dev)
+            if a_ptrs:
+                launches.append(stream_dgrad)
+        # one launch per stream (600 128x128 tiles each, under one round of the chip's resident
+        # slots): on their own streams the three overlap each other's last-round tails
+        if _PAR_STREAM_DGRAD:
+            streams.run_parallel(launches, dev)
+        else:
+            for f in launches:
+                f()
         ctx.state = None
         return (dY, None) + (None,) * len(params)
 

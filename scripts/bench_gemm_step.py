@@ -33,6 +33,10 @@ def make_shapes(R):
         ("wgrad b3 TN 512x512xR", 512, 512, R, False, False, 3, F32, {"beta": 1.0}),
         ("wgrad b3 TN 1536x512xR", 1536, 512, R, False, False, 3, F32, {"beta": 1.0}),
         ("attn dKdV b384 TN 300x512x300", 300, 512, 300, False, False, 384, BF16, {}),
+        ("attn dKdV b384 TN 300x512x320 (K padded)", 300, 512, 320, False, False, 384, BF16, {}),
+        ("attn dKdV b384 TN 320x512x320 (M, K padded)", 320, 512, 320, False, False, 384, BF16, {}),
+        ("attn dKdV b768 TN 300x512x300 (dK + dV)", 300, 512, 300, False, False, 768, BF16, {}),
+        ("attn dKdV b768 TN 300x512x320 (dK + dV, K padded)", 300, 512, 320, False, False, 768, BF16, {}),
         ("ca wgrad b6 TN 1024x512xR", 1024, 512, R, False, False, 6, F32, {"beta": 1.0}),
         ("ca wgrad b6 TN 512x512xR", 512, 512, R, False, False, 6, F32, {"beta": 1.0}),
         ("enc wgrad b3 TN 512x1536xR", 512, 1536, R, False, False, 3, F32, {"beta": 1.0}),
