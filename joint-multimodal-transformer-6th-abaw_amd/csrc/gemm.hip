@@ -114,6 +114,10 @@ using Cfg21 = TileCfg<128, 128, 2, 2, 64, 4, 1, 1, 0, 2, 1>;
 // up to 2x slower on larger launches: those launches sit on a ~15 us floor of launch, first-load
 // and store-drain latency, not on per-K-tile latency; profiles/r02_gemm_small_tiles_realdata.jsonl)
 // (without s_setprio the two measured the same: profiles/r01_gemm_occupancy.txt)
+// (an epilogue that issues the beta*C / ReLU-mask loads of ALL its rows before the first store, to
+// overlap their latencies: 8 B x TM x TN more live registers per lane — 62-133 VGPRs spilled on
+// the 256x256 and 128x128/64-B tiles and 3 -> 2 blocks/CU on the others (hipcc
+// -Rpass-analysis=kernel-resource-usage), so it was not run)
 // (8-wave 128x256 / 256x128 tiles with 64-B K-tiles, 3 stages, 2 blocks / CU measured 20-100%
 // slower on every step shape: profiles/r01_gemm_occupancy.txt)
 // (deeper pipelines — 256x256 KB=64 with 3-4 stages, 128x128 with 3-4 stages — measured 0-40%
