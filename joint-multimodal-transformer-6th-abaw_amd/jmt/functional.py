@@ -16,6 +16,7 @@ Layout conventions
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -404,6 +405,132 @@ class MLPFn(Function):
 
 def mlp(x, W1, b1, W2, b2, out_dtype=None):
     return MLPFn.apply(W1, b1, W2, b2, out_dtype, x)
+
+
+_pair_mlp = {"on": os.environ.get("JMT_PAIR_MLP", "1") != "0"}
+
+
+def pair_mlps_enabled() -> bool:
+    """Two_transformers runs its V / A regressors as one MLPPairFn (JMT_PAIR_MLP=0: two MLPFn)."""
+    return _pair_mlp["on"]
+
+
+def set_pair_mlps(on: bool) -> None:
+    _pair_mlp["on"] = bool(on)
+
+
+class MLPPairFn(Function):
+    """(MLP_a(x), MLP_b(x)) for two same-shaped MLPs on ONE input: the V and A regressors of
+    two_transformers.py:104-114,125-126 (dropout p = 0).  Per output element the arithmetic is
+    MLPFn's, with fewer launches: both first layers are one GEMM launch (a 2-entry weight / bias
+    table writing [h_a | h_b] side by side), their weight gradients one grouped wgrad launch and
+    their bias gradients one grouped column-sum; the input gradient is the two dgrads and the
+    same 16-bit add autograd performs for the two uses of x."""
+
+    @staticmethod
+    def forward(ctx, W1a, b1a, W2a, b2a, W1b, b1b, W2b, b2b, out_dtype, x):
+        cd = compute_dtype()
+        L = Rows(x, cd)
+        hid, nout = W1a.shape[0], W2a.shape[0]
+        h = L.like(2 * hid, cd)
+        ldh = _ld(h, L.perm)
+        Wa, Wb = weight_as(W1a, cd), weight_as(W1b, cd)
+        ops.gemm(M=L.rows, N=hid, K=L.F, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                 a=[L.t.data_ptr()], lda=L.ld, a_kmajor=True,
+                 b=[Wa.data_ptr(), Wb.data_ptr()], ldb=L.F, b_kmajor=True, b_mode=1,
+                 c=[h.data_ptr()], ldc=ldh, batch0=2, sA=(0, 0), sC=(hid, 0),
+                 bias_tab=[b1a, b1b], bias_mode=1, relu=True, device=h.device)
+        odt = out_dtype if out_dtype is not None else cd
+        ys = []
+        for half, W2, b2 in ((0, W2a, b2a), (1, W2b, b2b)):
+            y = L.like(nout, odt)
+            _linear_fwd([h[..., half * hid:(half + 1) * hid]], ldh, L.rows, hid, W2, 0, nout, b2,
+                        y, _ld(y, L.perm), cd)
+            ys.append(y)
+        ctx.save_for_backward(W1a, b1a, W2a, b2a, W1b, b1b, W2b, b2b, L.t, h)
+        ctx.meta = (cd, L, x.dtype, odt)
+        return ys[0], ys[1]
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gya, gyb):
+        W1a, b1a, W2a, b2a, W1b, b1b, W2b, b2b, xin, h = ctx.saved_tensors
+        cd, L, xdt, odt = ctx.meta
+        hid, nout = W1a.shape[0], W2a.shape[0]
+        dev = h.device
+        ldh = _ld(h, L.perm)
+        hs = (h[..., :hid], h[..., hid:])
+        dh = L.like(2 * hid, cd)
+        dhs = (dh[..., :hid], dh[..., hid:])
+        gys = []
+        for gy in (gya, gyb):
+            if gy is None:
+                gy = torch.zeros(L.like(nout, odt).shape, dtype=odt, device=dev)
+            gys.append(gy)
+        for gy, W2, hp, dhp in zip(gys, (W2a, W2b), hs, dhs):
+            Gy = _match(gy, Rows(L.like(nout, cd)), cd)
+            _dgrad(Gy, nout, W2, 0, cd, [dhp], ldh, 1, hid, aux=hp, ldaux=ldh)
+
+        def w2_grads():         # side stream (jmt.streams.run_side), as in MLPFn
+            if odt == torch.float32 and cd != torch.float32 and nout <= 16:
+                h32 = _cast_keep_layout(h, torch.float32)
+                l32 = _ld(h32, L.perm)
+                for gy, W2, b2, half in zip(gys, (W2a, W2b), (b2a, b2b), (0, 1)):
+                    G32 = _match(gy, Rows(L.like(nout, torch.float32)), torch.float32)
+                    _wgrad(G32, nout, [h32[..., half * hid:(half + 1) * hid]], l32, hid, W2, 0,
+                           torch.float32)
+                    _bgrad(G32, nout, b2, 0)
+            else:
+                for gy, W2, b2, hp in zip(gys, (W2a, W2b), (b2a, b2b), hs):
+                    Gy = _match(gy, Rows(L.like(nout, cd)), cd)
+                    _wgrad(Gy, nout, [hp], ldh, hid, W2, 0, cd)
+                    _bgrad(Gy, nout, b2, 0)
+
+        streams.run_side(w2_grads, reads=(gya, gyb, h))
+        dx = None
+        if ctx.needs_input_grad[9]:
+            dx = L.like(L.F, cd)
+            ldx = _ld(dx, L.perm)
+            dxb = L.like(L.F, cd)
+            _dgrad(Rows(dhs[0]), hid, W1a, 0, cd, [dx], ldx, 1, L.F)
+            _dgrad(Rows(dhs[1]), hid, W1b, 0, cd, [dxb], _ld(dxb, L.perm), 1, L.F)
+            # the sum of the two input gradients rounded as autograd rounds it (a beta = 1
+            # accumulate in the second dgrad saves this add but rounds once less, which moved an
+            # fp16 gradient of the H8/L2 golden case 0.02 % past the error model's bound)
+            dx.add_(dxb)
+            if xdt != cd:
+                dx = _cast_keep_layout(dx, xdt)
+
+        def w1_grads():         # one grouped wgrad launch + one grouped column-sum launch pair
+            gws = []
+            for W in (W1a, W1b):
+                g = _grad_buffer(W)
+                gws.append(g if g is not None else torch.zeros_like(W))
+            ops.gemm(M=hid, N=L.F, K=L.rows, ab_dtype=_dc(cd), c_dtype=F32,
+                     a=[dh.data_ptr()], lda=ldh, a_kmajor=False,
+                     b=[xin.data_ptr()], ldb=L.ld, b_kmajor=False,
+                     c=[g.data_ptr() for g in gws], ldc=L.F, c_mode=1, batch0=2,
+                     sA=(hid, 0), sB=(0, 0), beta=1.0, device=dev)
+            _grad_done(W1a, W1b)
+            dbs = []
+            for b in (b1a, b1b):
+                gb = _grad_buffer(b)
+                dbs.append(gb if gb is not None else torch.empty(hid, dtype=torch.float32,
+                                                                 device=dev))
+            ops.colsum_grouped(dh.data_ptr(), _dc(cd), 2, ldh, hid, L.rows, hid, dbs,
+                               beta_acc=True, device=dev)
+            _grad_done(b1a, b1b)
+
+        streams.run_side(w1_grads, reads=(dh, xin))
+        return (None,) * 9 + (dx,)
+
+
+def mlp_pair(x, mlp_a, mlp_b, out_dtype=None):
+    """Both regressor MLPs (jmt.nn.MLP: Linear, ReLU, [Dropout p=0], Linear) on the same x."""
+    la1, la2 = mlp_a[0], mlp_a[len(mlp_a) - 1]
+    lb1, lb2 = mlp_b[0], mlp_b[len(mlp_b) - 1]
+    return MLPPairFn.apply(la1.weight, la1.bias, la2.weight, la2.bias, lb1.weight, lb1.bias,
+                           lb2.weight, lb2.bias, out_dtype, x)
 
 
 # ------------------------------------------------------------------------- L2 normalize

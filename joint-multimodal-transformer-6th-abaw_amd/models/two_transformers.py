@@ -86,8 +86,16 @@ class Two_transformers(nn.Module):
         taps.record("head", av, self.joint_modalities == 'TRANSFORMER' and
                     self.output_format == 'FC')
         # regressors in fp32 out (predictions feed the fp32 CCC statistics)
-        vouts = self.vregressor(av, out_dtype=torch.float32).squeeze(2)
-        aouts = self.aregressor(av, out_dtype=torch.float32).squeeze(2)
+        vr, ar = self.vregressor, self.aregressor
+        if (F.pair_mlps_enabled() and not ((vr._p or ar._p) and self.training)
+                and vr[0].weight.shape == ar[0].weight.shape):
+            # both regressors read av: one MLP-pair function (fewer launches, same arithmetic
+            # per output element as the two MLP calls below)
+            vouts, aouts = F.mlp_pair(av, vr, ar, out_dtype=torch.float32)
+            vouts, aouts = vouts.squeeze(2), aouts.squeeze(2)
+        else:
+            vouts = vr(av, out_dtype=torch.float32).squeeze(2)
+            aouts = ar(av, out_dtype=torch.float32).squeeze(2)
         if vouts.dim() == 2 and not vouts.is_contiguous():   # seq-first (T,B) -> contiguous
             vouts = F.TransposeCopyFn.apply(vouts)
             aouts = F.TransposeCopyFn.apply(aouts)
