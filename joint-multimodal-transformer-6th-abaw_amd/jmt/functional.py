@@ -422,10 +422,12 @@ def set_pair_mlps(on: bool) -> None:
 class MLPPairFn(Function):
     """(MLP_a(x), MLP_b(x)) for two same-shaped MLPs on ONE input: the V and A regressors of
     two_transformers.py:104-114,125-126 (dropout p = 0).  Per output element the arithmetic is
-    MLPFn's, with fewer launches: both first layers are one GEMM launch (a 2-entry weight / bias
-    table writing [h_a | h_b] side by side), their weight gradients one grouped wgrad launch and
-    their bias gradients one grouped column-sum; the input gradient is the two dgrads and the
-    same 16-bit add autograd performs for the two uses of x."""
+    MLPFn's, with half the launches: both first layers are one GEMM launch (a 2-entry weight /
+    bias table writing [h_a | h_b] side by side), both second layers one launch over the halves
+    of h, and in the backward both second-layer input gradients, both second-layer and both
+    first-layer weight gradients are one launch each, both first-layer bias gradients one grouped
+    column sum; the input gradient is the two dgrads and the same 16-bit add autograd performs
+    for the two uses of x."""
 
     @staticmethod
     def forward(ctx, W1a, b1a, W2a, b2a, W1b, b1b, W2b, b2b, out_dtype, x):
@@ -441,15 +443,38 @@ class MLPPairFn(Function):
                  c=[h.data_ptr()], ldc=ldh, batch0=2, sA=(0, 0), sC=(hid, 0),
                  bias_tab=[b1a, b1b], bias_mode=1, relu=True, device=h.device)
         odt = out_dtype if out_dtype is not None else cd
-        ys = []
-        for half, W2, b2 in ((0, W2a, b2a), (1, W2b, b2b)):
-            y = L.like(nout, odt)
-            _linear_fwd([h[..., half * hid:(half + 1) * hid]], ldh, L.rows, hid, W2, 0, nout, b2,
-                        y, _ld(y, L.perm), cd)
-            ys.append(y)
+        # both second layers: one launch over the halves of h (2-entry weight / bias / out table)
+        ys = [L.like(nout, odt), L.like(nout, odt)]
+        W2c = [weight_as(W2a, cd), weight_as(W2b, cd)]
+        ops.gemm(M=L.rows, N=nout, K=hid, ab_dtype=_dc(cd), c_dtype=_dc(odt),
+                 a=[h.data_ptr()], lda=ldh, a_kmajor=True, sA=(hid, 0),
+                 b=[w.data_ptr() for w in W2c], ldb=hid, b_kmajor=True, b_mode=1,
+                 c=[y.data_ptr() for y in ys], ldc=_ld(ys[0], L.perm), c_mode=1, batch0=2,
+                 bias_tab=[b2a, b2b], bias_mode=1, device=h.device)
         ctx.save_for_backward(W1a, b1a, W2a, b2a, W1b, b1b, W2b, b2b, L.t, h)
         ctx.meta = (cd, L, x.dtype, odt)
         return ys[0], ys[1]
+
+    @staticmethod
+    def _w2_grads(Gs, hh, ldhh, hid, nout, W2s, b2s, dt, dev):
+        """W2_g.grad += G_g^T h_g (both in one launch when the gradients share a row stride),
+        b2_g.grad += column sums of G_g."""
+        gWs = [_grad_buffer(W) for W in W2s]
+        if nout == 1 or Gs[0].ld == Gs[1].ld:
+            a_ld, a_kmaj = (Gs[0].ld, False) if nout > 1 else (_vec(dt), True)
+            if all(g is not None for g in gWs):
+                ops.gemm(M=nout, N=hid, K=Gs[0].rows, ab_dtype=_dc(dt), c_dtype=F32,
+                         a=[G.t.data_ptr() for G in Gs], lda=a_ld, a_kmajor=a_kmaj, a_mode=1,
+                         b=[hh.data_ptr()], ldb=ldhh, b_kmajor=False, sB=(hid, 0),
+                         c=[g.data_ptr() for g in gWs], ldc=hid, c_mode=1, batch0=2, beta=1.0,
+                         device=dev)
+                _grad_done(*W2s)
+                gWs = None
+        if gWs is not None:
+            for half, (G, W2) in enumerate(zip(Gs, W2s)):
+                _wgrad(G, nout, [hh[..., half * hid:(half + 1) * hid]], ldhh, hid, W2, 0, dt)
+        for G, b2 in zip(Gs, b2s):
+            _bgrad(G, nout, b2, 0)
 
     @staticmethod
     @once_differentiable
@@ -467,26 +492,31 @@ class MLPPairFn(Function):
             if gy is None:
                 gy = torch.zeros(L.like(nout, odt).shape, dtype=odt, device=dev)
             gys.append(gy)
-        for gy, W2, hp, dhp in zip(gys, (W2a, W2b), hs, dhs):
-            Gy = _match(gy, Rows(L.like(nout, cd)), cd)
-            _dgrad(Gy, nout, W2, 0, cd, [dhp], ldh, 1, hid, aux=hp, ldaux=ldh)
+        Gys = [_match(gy, Rows(L.like(nout, cd)), cd) for gy in gys]
+        if nout == 1 or Gys[0].ld == Gys[1].ld:
+            # both second-layer input gradients (ReLU-masked) in one launch into [dh_a | dh_b]
+            a_ld, a_kmaj = (_vec(cd), False) if nout == 1 else (Gys[0].ld, True)
+            W2c = [weight_as(W2a, cd), weight_as(W2b, cd)]
+            ops.gemm(M=L.rows, N=hid, K=nout, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                     a=[G.t.data_ptr() for G in Gys], lda=a_ld, a_kmajor=a_kmaj, a_mode=1,
+                     b=[w.data_ptr() for w in W2c], ldb=hid, b_kmajor=False, b_mode=1,
+                     c=[dh.data_ptr()], ldc=ldh, batch0=2, sC=(hid, 0), aux=h, ldaux=ldh,
+                     device=dev)
+        else:
+            for Gy, W2, hp, dhp in zip(Gys, (W2a, W2b), hs, dhs):
+                _dgrad(Gy, nout, W2, 0, cd, [dhp], ldh, 1, hid, aux=hp, ldaux=ldh)
 
         def w2_grads():         # side stream (jmt.streams.run_side), as in MLPFn
             if odt == torch.float32 and cd != torch.float32 and nout <= 16:
                 h32 = _cast_keep_layout(h, torch.float32)
-                l32 = _ld(h32, L.perm)
-                for gy, W2, b2, half in zip(gys, (W2a, W2b), (b2a, b2b), (0, 1)):
-                    G32 = _match(gy, Rows(L.like(nout, torch.float32)), torch.float32)
-                    _wgrad(G32, nout, [h32[..., half * hid:(half + 1) * hid]], l32, hid, W2, 0,
-                           torch.float32)
-                    _bgrad(G32, nout, b2, 0)
+                G32 = [_match(gy, Rows(L.like(nout, torch.float32)), torch.float32)
+                       for gy in gys]
+                MLPPairFn._w2_grads(G32, h32, _ld(h32, L.perm), hid, nout, (W2a, W2b),
+                                    (b2a, b2b), torch.float32, dev)
             else:
-                for gy, W2, b2, hp in zip(gys, (W2a, W2b), (b2a, b2b), hs):
-                    Gy = _match(gy, Rows(L.like(nout, cd)), cd)
-                    _wgrad(Gy, nout, [hp], ldh, hid, W2, 0, cd)
-                    _bgrad(Gy, nout, b2, 0)
+                MLPPairFn._w2_grads(Gys, h, ldh, hid, nout, (W2a, W2b), (b2a, b2b), cd, dev)
 
-        streams.run_side(w2_grads, reads=(gya, gyb, h))
+        streams.run_side(w2_grads, reads=(gya, gyb, h) + tuple(G.t for G in Gys))
         dx = None
         if ctx.needs_input_grad[9]:
             dx = L.like(L.F, cd)
