@@ -1042,6 +1042,9 @@ static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, in
   if (!ak && !bk && batch >= 64 && M <= 512 && N <= 512 && K >= 128 && K <= 512)
     return 11;                                                   // attn dK / dV
   if (ak && !bk && batch == 1 && K >= 3072) return 11;           // K-concat stream dgrad
+  if (ak && !bk && batch == 1 && K <= 128 && M >= 4096 && N >= 512)
+    return 11;         // short-K dgrad (the regressors' first layer, K = 128): 28.7 -> 23.3 us,
+                       // profiles/r02_regressor_gemm_sweep.jsonl
   if (ak && !bk && batch >= 3 && batch <= 8 && K >= 512 && M >= 4096 && N >= 512)
     return 20;                                                   // grouped / head dgrads
   if (ak && bk && batch >= 3 && K == 512 && M >= 4096 && N >= 512) return 5;   // grouped fwd

@@ -33,6 +33,9 @@ def make_shapes(R):
         ("wgrad b3 TN 512x512xR", 512, 512, R, False, False, 3, F32, {"beta": 1.0}),
         ("wgrad b3 TN 1536x512xR", 1536, 512, R, False, False, 3, F32, {"beta": 1.0}),
         ("attn dKdV b384 TN 300x512x300", 300, 512, 300, False, False, 384, BF16, {}),
+        ("regressor dgrad NN 1024x128", R, 1024, 128, True, False, 1, BF16, {}),
+        ("regressor dgrad NN 1024x128 beta", R, 1024, 128, True, False, 1, BF16, {"beta": 1.0}),
+        ("regressor fwd pair NT 128x1024 relu", R, 128, 1024, True, True, 2, BF16, {"sA0": True}),
         ("attn dKdV b384 TN 300x512x320 (K padded)", 300, 512, 320, False, False, 384, BF16, {}),
         ("attn dKdV b384 TN 320x512x320 (M, K padded)", 320, 512, 320, False, False, 384, BF16, {}),
         ("attn dKdV b768 TN 300x512x300 (dK + dV)", 300, 512, 300, False, False, 768, BF16, {}),
