@@ -82,22 +82,35 @@ def step_flops(B: int, T: int, Da: int = D_A, Dv: int = D_V, fc: bool = True,
     """Algorithmic matmul FLOPs of one training step (SURVEY.md §8d closed form for
     TRANSFORMER/FC, L=1, h=d): F per window = input projections + out_layer_pv + 3 encoders +
     6 cross-attentions + out_layer1 + regressors; W = 3F minus the input gradients of the
-    projections that act on leaf inputs.  SELF_ATTEN swaps out_layer1 for its head.  None for
-    joint_modalities other than TRANSFORMER."""
-    if jm != "TRANSFORMER" or fmt not in ("FC", "SELF_ATTEN"):
-        return None
+    projections that act on leaf inputs.  SELF_ATTEN swaps out_layer1 for its head.
+    NONE (MultimodalTransformer_wo_JR, mm_transformers.py:119-146): 2 encoders whose
+    self-attention runs over the BATCH axis (a length-B sequence per time step: 4 B d FLOP per
+    token), 2 cross-attentions over T, final_layer 1024->512, regressors over 512.
+    FC (FeatureConcatFC, mm_multi_transformers.py:217-224): one 1024->512 linear + regressors."""
     d = E
     proj = (2 * T * d * Da if fc else 0) + (2 * T * d * Dv if Dv != 512 else 0)
+    reg = lambda dim: 4 * T * dim * 128 + 4 * T * 128 * k          # V and A regressors
+    if jm == "NONE" and fmt == "FC":
+        F = (proj + 2 * (12 * T * d * d + 4 * T * B * d) + 2 * (8 * T * d * d + 4 * T * T * d)
+             + 4 * T * d * d + reg(512))
+        leaf = proj if proj else 12 * T * d * d       # else: the encoders' qkv input gradients
+        return (3 * F - leaf) * B
+    if jm == "FC" and fmt == "FC":
+        F = proj + 4 * T * d * d + reg(512)
+        leaf = proj if proj else 4 * T * d * d
+        return (3 * F - leaf) * B
+    if jm != "TRANSFORMER" or fmt not in ("FC", "SELF_ATTEN"):
+        return None
     F = (proj + 4 * T * d * d + 3 * (12 * T * d * d + 4 * T * T * d)
-         + 6 * (8 * T * d * d + 4 * T * T * d) + 4 * T * 128 * k)
+         + 6 * (8 * T * d * d + 4 * T * T * d))
     if fmt == "FC":
-        F += 24 * T * d * d + 4 * T * 1024 * 128             # out_layer1 + regressors (1024)
+        F += 24 * T * d * d + reg(1024)               # out_layer1 + regressors (1024)
     else:
         # SELF_ATTEN head (mm_multi_transformers.py:169-199): an encoder layer over the 6
         # cross-attention outputs of every clip, then MHA with the last token as the only query
         # row that is kept (q: 1 token, k/v: 6 tokens, out_proj: 1 token); regressors over 512
         F += 6 * T * (12 * d * d + 4 * 6 * d) + T * (2 * d * d + 24 * d * d + 4 * 6 * d
-                                                    + 2 * d * d) + 4 * T * 512 * 128
+                                                    + 2 * d * d) + reg(512)
     leaf = proj if proj else 4 * T * d * d + 2 * 6 * T * d * d
     return (3 * F - leaf) * B
 
@@ -265,9 +278,11 @@ def cpu_baseline(model_sd, fc_sd, audio, video, lv, la, steps=2):
     t = sum(times[1:]) / steps
     return {"value": round(B / t, 3), "unit": "windows/s", "cores": threads, "kind": "port",
             "sample": f"oracle/jmt_ref.py train_step on the bench batch (B={B} T={T}, rank 0's "
-                      f"data, initial weights), fp32 torch-CPU, {threads} threads (affinity set "
-                      f"{aff} CPUs; OMP_NUM_THREADS = the box's share), 1 warm-up + {steps} timed "
-                      f"steps ({t * 1e3:.0f} ms/step)"}
+                      f"data, initial weights), fp32 torch-CPU, {threads} threads, 1 warm-up + "
+                      f"{steps} timed steps ({t * 1e3:.0f} ms/step)",
+            "threads_policy": f"{threads} = OMP_NUM_THREADS, the CPU share the GPU pool gives one "
+                              f"GPU's job; the affinity mask ({aff} CPUs) is the whole host, "
+                              "shared with the other GPU slots, so it is not used"}
 
 
 def main():
@@ -434,7 +449,11 @@ def main():
 
     run = step
     graphed = None
-    use_graph = args.graph and (world == 1 or os.environ.get("JMT_GRAPH_DIST", "0") == "1")
+    # N > 1 captures the RCCL all-reduces (per bucket, on the communication stream) and the CCC
+    # statistics all-gather into the graph as well (tests/test_gpu_dist.py
+    # test_rccl_bucketed_step_sync_free_and_capturable): the eager step is host-bound (its issue
+    # time, host_issue_ms_per_eager_step, is about the GPU step time).  JMT_GRAPH_DIST=0 = eager.
+    use_graph = args.graph and (world == 1 or os.environ.get("JMT_GRAPH_DIST", "1") == "1")
     if use_graph:
         # the whole step as one hipGraph (jmt/graph.py): replay issues ~300 launches at once
         graphed = GraphedStep(step).capture(warmup=1)

@@ -226,6 +226,22 @@ int jmt_ccc_finish(int kind, int world, const double* stats_all, int64_t bs, flo
 int jmt_ccc_bwd(int kind, int pred_dt, int64_t n, int k, const void* pred, const float* label,
                 float ignore, float lo, float hi, const double* coef, const float* grad_loss,
                 void* dpred, void* stream);
+/* CELoss (losses/loss.py:34-51; replaces its host numpy digitize + F.cross_entropy): labels
+ * digitized on the device into k bins (np.digitize over linspace(lo, hi, k + 1) - 1, top bin
+ * clamped), x (n, k) logits, optional class weights (k floats, NULL = none).
+ * jmt_ce_stats: double[4] = (sum w nll, sum w, labels below lo, 0) of this rank's rows;
+ * jmt_ce_finish: `world` ranks' stats (rank order) -> loss = sum w nll / sum w (fp32 scalar; NaN
+ * when any label fell below lo, where the reference raises) and coef[0] = 1 / sum w;
+ * jmt_ce_bwd: dx_ij = grad_loss w[c_i] coef[0] (softmax(x_i)_j - [j == c_i]);
+ * jmt_ce_labels: the digitized labels (int64).  No host synchronisation. */
+int jmt_ce_stats(int x_dt, int64_t n, int k, const void* x, const float* label, float lo, float hi,
+                 const float* weights, double* stats, void* stream);
+int jmt_ce_finish(int world, const double* stats_all, float* loss, double* coef, void* stream);
+int jmt_ce_bwd(int x_dt, int64_t n, int k, const void* x, const float* label, float lo, float hi,
+               const float* weights, const double* coef, const float* grad_loss, void* dx,
+               void* stream);
+int jmt_ce_labels(int64_t n, int k, const float* label, float lo, float hi, int64_t* out,
+                  void* stream);
 /* Mask indices (labels != ignore) in ascending order, count written to *count (device int64).
  * The bit-exact padding-mask indices of the ignore path. */
 int jmt_mask_indices(int64_t n, const float* label, float ignore, int64_t* idx, int64_t* count,

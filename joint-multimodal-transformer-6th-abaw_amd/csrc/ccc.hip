@@ -275,9 +275,166 @@ __global__ __launch_bounds__(CT) void mask_indices_kernel(int64_t n, const float
   if (threadIdx.x == 0) *count = base;
 }
 
+// ---- CELoss (losses/loss.py:34-51): labels digitized on the device -----------------------------
+// np.digitize(y, linspace(lo, hi, k + 1)) - 1 with the top bin clamped (loss.py:44-48): the bin
+// is (number of edges <= y) - 1, edges in float64 as numpy builds them (i * step + lo, the last
+// = hi); NaN -> k - 1 (numpy gives len(edges)).  A label below lo gives bin -1, on which the
+// reference's F.cross_entropy raises: here it is counted (stats[2]) and the loss is NaN.
+__device__ __forceinline__ int ce_bin(float yf, int k, float lo, float hi) {
+  if (yf != yf) return k - 1;
+  const double y = (double)yf, step = ((double)hi - (double)lo) / (double)k;
+  int c = 0;
+  for (int j = 0; j <= k; ++j) {
+    const double e = j == k ? (double)hi : (double)j * step + (double)lo;
+    c += e <= y;
+  }
+  c -= 1;
+  return c == k ? k - 1 : c;
+}
+
+// one block: per row nll = logsumexp(x_i) - x_i[c_i], weight w[c_i] (1 without weights);
+// stats = (sum w nll, sum w, invalid labels, 0) in double, rows in a fixed order per thread
+template <typename T>
+__global__ __launch_bounds__(CT) void ce_stats_kernel(int64_t n, int k, const T* x,
+                                                      const float* label, float lo, float hi,
+                                                      const float* wts, double* stats) {
+  __shared__ double red[3 * (CT / 64)];
+  double sl = 0, sw = 0, bad = 0;
+  for (int64_t i = threadIdx.x; i < n; i += CT) {
+    const int c = ce_bin(label[i], k, lo, hi);
+    if (c < 0) {
+      bad += 1.0;
+      continue;
+    }
+    const T* z = x + i * k;
+    float m = -INFINITY;
+    for (int j = 0; j < k; ++j) m = fmaxf(m, to_f(z[j]));
+    float s = 0.f;
+    for (int j = 0; j < k; ++j) s += __expf(to_f(z[j]) - m);
+    const double nll = (double)(m + __logf(s) - to_f(z[c]));
+    const double w = wts ? (double)wts[c] : 1.0;
+    sl += w * nll;
+    sw += w;
+  }
+  block_sum3_d(sl, sw, bad, red);
+  if (threadIdx.x == 0) {
+    stats[0] = sl;
+    stats[1] = sw;
+    stats[2] = bad;
+    stats[3] = 0.0;
+  }
+}
+
+// world ranks' stats (rank order) -> loss = sum w nll / sum w (NaN on an invalid label) and
+// coef[0] = 1 / sum w for the backward
+__global__ void ce_finish_kernel(int world, const double* stats_all, float* loss, double* coef) {
+  if (threadIdx.x != 0) return;
+  double sl = 0, sw = 0, bad = 0;
+  for (int r = 0; r < world; ++r) {
+    sl += stats_all[4 * r];
+    sw += stats_all[4 * r + 1];
+    bad += stats_all[4 * r + 2];
+  }
+  *loss = bad > 0 ? __builtin_nanf("") : (float)(sl / sw);
+  coef[0] = bad > 0 ? __builtin_nan("") : 1.0 / sw;
+}
+
+// dx_ij = grad_loss * w[c_i] / sum w * (softmax(x_i)_j - [j == c_i])
+template <typename T>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(int64_t n, int k, const T* x,
+                                                     const float* label, float lo, float hi,
+                                                     const float* wts, const double* coef,
+                                                     const float* grad_loss, T* dx) {
+  const double inv = coef[0];
+  const float g = grad_loss ? *grad_loss : 1.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = ce_bin(label[i], k, lo, hi);
+    const T* z = x + i * k;
+    T* dz = dx + i * k;
+    const float sc = c < 0 ? __builtin_nanf("")
+                           : (float)((wts ? (double)wts[c] : 1.0) * inv * (double)g);
+    float m = -INFINITY;
+    for (int j = 0; j < k; ++j) m = fmaxf(m, to_f(z[j]));
+    float s = 0.f;
+    float pv[MAXK];
+    for (int j = 0; j < k; ++j) {
+      pv[j] = __expf(to_f(z[j]) - m);
+      s += pv[j];
+    }
+    const float is = 1.f / s;
+    for (int j = 0; j < k; ++j) dz[j] = from_f<T>(sc * (pv[j] * is - (j == c ? 1.f : 0.f)));
+  }
+}
+
+// the digitized labels themselves (int64, as the reference's torch.cuda.LongTensor(y_dig))
+__global__ void ce_labels_kernel(int64_t n, int k, const float* label, float lo, float hi,
+                                 int64_t* out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = ce_bin(label[i], k, lo, hi);
+}
+
 }  // namespace jmt
 
 using namespace jmt;
+
+#define JMT_CE_DISPATCH(name, KER, GRID, BLK, ...)                                         \
+  switch (x_dt) {                                                                          \
+    case JMT_F32: hipLaunchKernelGGL((KER<float>), GRID, BLK, 0, st, __VA_ARGS__(float)); break; \
+    case JMT_BF16: hipLaunchKernelGGL((KER<__bf16>), GRID, BLK, 0, st, __VA_ARGS__(__bf16)); break; \
+    case JMT_F16: hipLaunchKernelGGL((KER<_Float16>), GRID, BLK, 0, st, __VA_ARGS__(_Float16)); break; \
+    default: return set_error(JMT_ERR_ARG, name ": dtype");                                 \
+  }
+
+extern "C" int jmt_ce_stats(int x_dt, int64_t n, int k, const void* x, const float* label,
+                            float lo, float hi, const float* weights, double* stats,
+                            void* stream) {
+  JMT_CHECK_ARG(k >= 2 && k <= MAXK, "jmt_ce_stats: digitize_num %d unsupported", k);
+  JMT_CHECK_ARG(stats && (n == 0 || (x && label)), "jmt_ce_stats: null pointer");
+  hipStream_t st = as_stream(stream);
+#define ARGS(T) n, k, (const T*)x, label, lo, hi, weights, stats
+  JMT_CE_DISPATCH("jmt_ce_stats", ce_stats_kernel, dim3(1), dim3(CT), ARGS)
+#undef ARGS
+  JMT_LAUNCH_CHECK("jmt_ce_stats");
+  return JMT_OK;
+}
+
+extern "C" int jmt_ce_finish(int world, const double* stats_all, float* loss, double* coef,
+                             void* stream) {
+  JMT_CHECK_ARG(world >= 1 && stats_all && loss && coef, "jmt_ce_finish: bad args");
+  hipLaunchKernelGGL(ce_finish_kernel, dim3(1), dim3(64), 0, as_stream(stream), world,
+                     stats_all, loss, coef);
+  JMT_LAUNCH_CHECK("jmt_ce_finish");
+  return JMT_OK;
+}
+
+extern "C" int jmt_ce_bwd(int x_dt, int64_t n, int k, const void* x, const float* label,
+                          float lo, float hi, const float* weights, const double* coef,
+                          const float* grad_loss, void* dx, void* stream) {
+  if (n == 0) return JMT_OK;
+  JMT_CHECK_ARG(k >= 2 && k <= MAXK && x && label && coef && dx, "jmt_ce_bwd: bad args");
+  hipStream_t st = as_stream(stream);
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+#define ARGS(T) n, k, (const T*)x, label, lo, hi, weights, coef, grad_loss, (T*)dx
+  JMT_CE_DISPATCH("jmt_ce_bwd", ce_bwd_kernel, dim3(blocks), dim3(256), ARGS)
+#undef ARGS
+  JMT_LAUNCH_CHECK("jmt_ce_bwd");
+  return JMT_OK;
+}
+
+extern "C" int jmt_ce_labels(int64_t n, int k, const float* label, float lo, float hi,
+                             int64_t* out, void* stream) {
+  if (n == 0) return JMT_OK;
+  JMT_CHECK_ARG(k >= 2 && k <= MAXK && label && out, "jmt_ce_labels: bad args");
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(ce_labels_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), n, k,
+                     label, lo, hi, out);
+  JMT_LAUNCH_CHECK("jmt_ce_labels");
+  return JMT_OK;
+}
 
 extern "C" int jmt_ccc_stats(int kind, int pred_dt, int64_t n, int k, const void* pred,
                              const float* label, float ignore, float lo, float hi, double* stats,

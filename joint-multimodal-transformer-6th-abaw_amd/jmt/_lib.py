@@ -97,6 +97,11 @@ _PROTOS = {
     "jmt_mask_indices": (c_int, [c_i64, c_vp, c_f, c_vp, c_vp, c_vp]),
     "jmt_vp_scatter": (c_int, [c_i64] + [c_vp] * 9 + [c_f, c_i64] + [c_vp] * 6),
     "jmt_vp_smooth": (c_int, [c_i64, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "jmt_ce_stats": (c_int, [c_int, c_i64, c_int, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp]),
+    "jmt_ce_finish": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp]),
+    "jmt_ce_bwd": (c_int, [c_int, c_i64, c_int, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_vp,
+                           c_vp]),
+    "jmt_ce_labels": (c_int, [c_i64, c_int, c_vp, c_f, c_f, c_vp, c_vp]),
     "jmt_vp_ccc": (c_int, [c_i64] + [c_vp] * 6),
     "jmt_amp_check": (c_int, [c_i64, c_vp, c_vp, c_vp]),
     "jmt_sgd_step_amp": (c_int, [c_i64, c_vp, c_vp, c_vp, c_f, c_f, c_f, c_f, c_int, c_int, c_vp,

@@ -137,24 +137,33 @@ class GradBucketer:
         self._hooks = [p.register_post_accumulate_grad_hook(lambda p: F._grad_done(p))
                        for p in opt.params]
         self.launch_log = []
+        # collectives also at world size 1 (tests: RCCL inside a captured step on a 1-GPU box)
+        self.world1 = False
 
     def begin(self):
         self._main = torch.cuda.current_stream() if self.cuda else None
         self.left = dict(self.expected)
         self.bucket_left = [b[2] for b in self.buckets]
         self.launched = [False] * len(self.buckets)
+        # streams that enqueued a write of each bucket's parameters (the compute stream, the
+        # weight-gradient side stream, the run_parallel branch streams, ...): the bucket's
+        # all-reduce is ordered after ALL of them, not only after the stream of its last write
+        self.writers = [[] for _ in self.buckets]
         self.works = []
         self.launch_log = []
         self._F._grad_hook = self._done
 
     def _done(self, ps):
+        cur = torch.cuda.current_stream() if self.cuda else None
         for p in ps:
             k = id(p)
             if k not in self.left:
                 continue
+            b = self.bucket_of[k]
+            if cur is not None and cur not in self.writers[b]:
+                self.writers[b].append(cur)
             self.left[k] -= 1
             if self.left[k] == 0:
-                b = self.bucket_of[k]
                 self.bucket_left[b] -= 1
                 if self.bucket_left[b] == 0:
                     self._launch(b)
@@ -166,19 +175,22 @@ class GradBucketer:
         self.launched[b] = True
         self.launch_log.append(b)
         lo, hi, _ = self.buckets[b]
-        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+        if not dist.is_initialized() or (dist.get_world_size(self.group) == 1 and
+                                         not self.world1):
             return
         if self.cuda:
-            ev = torch.cuda.Event()
-            ev.record()                                   # after the bucket's last write
-            self.comm.wait_event(ev)
-            # writes enqueued on the weight-gradient side stream (jmt.streams.run_side) and on
-            # the compute stream both precede the bucket's all-reduce
+            # every stream that wrote one of the bucket's gradients (recorded by _done), the
+            # stream this last notification came from, the weight-gradient side stream
+            # (jmt.streams.run_side) and the step's compute stream precede the all-reduce; a
+            # wait is one event record + one stream wait, no host synchronisation
             from . import streams
             cur = torch.cuda.current_stream()
-            for st in streams.side_streams() + [self._main]:
-                if st is not None and st != cur and st.device == cur.device:
-                    self.comm.wait_stream(st)
+            waits = list(self.writers[b])
+            for st in [cur] + streams.side_streams() + [self._main]:
+                if st is not None and st.device == cur.device and st not in waits:
+                    waits.append(st)
+            for st in waits:
+                self.comm.wait_stream(st)
             with torch.cuda.stream(self.comm):
                 self.works.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM,
                                                   group=self.group, async_op=True))

@@ -516,7 +516,7 @@ class MLPPairFn(Function):
             else:
                 MLPPairFn._w2_grads(Gys, h, ldh, hid, nout, (W2a, W2b), (b2a, b2b), cd, dev)
 
-        streams.run_side(w2_grads, reads=(gya, gyb, h) + tuple(G.t for G in Gys))
+        streams.run_side(w2_grads, reads=tuple(gys) + (h,) + tuple(G.t for G in Gys))
         dx = None
         if ctx.needs_input_grad[9]:
             dx = L.like(L.F, cd)
@@ -624,10 +624,16 @@ class AddLayerNormFn(Function):
         db = _grad_buffer(beta)
         tmp = None
         if dg is None or db is None:
-            tmp = torch.empty(2, L.F, dtype=torch.float32, device=x.device)
+            # one accumulate flag for both outputs: with a buffer missing both go to scratch and
+            # the present one accumulates it (gradient accumulation stays intact)
+            tmp = torch.zeros(2, L.F, dtype=torch.float32, device=x.device)
         ops.layernorm_bwd(x, L.ld, r, ldr, G.t, G.ld, mean, rstd, gamma, dx, _ld(dx, L.perm),
-                          dg if dg is not None else tmp[0], db if db is not None else tmp[1],
-                          True if tmp is None else False, L.rows, L.F)
+                          dg if tmp is None else tmp[0], db if tmp is None else tmp[1],
+                          tmp is None, L.rows, L.F)
+        if tmp is not None:
+            for b, t in ((dg, tmp[0]), (db, tmp[1])):
+                if b is not None:
+                    b.add_(t)
         _grad_done(gamma, beta)
         dxx = dx if xdt == cd else _cast_keep_layout(dx, xdt)
         drr = None
@@ -790,12 +796,25 @@ def attn_backward(saved, go, dq, dk, dv):
         go = go.clone(memory_format=torch.contiguous_format)
         so_l, so_n = go.stride(0), go.stride(1)
     if fused == "small":
+        # the kernel's layout contract covers the gradient buffers too: a misaligned one is
+        # written through an aligned (contiguous) temporary and copied back.  Aliased buffers
+        # (packed qkv) share one temporary.
+        outs, tmps = [], {}
+        for buf, col in ((dq, qcol), (dk, kcol), (dv, vcol)):
+            if _small_aligned(buf, col, cd):
+                outs.append((buf, col))
+                continue
+            key = id(buf)
+            if key not in tmps:
+                tmps[key] = (buf, buf.clone(memory_format=torch.contiguous_format))
+            outs.append((tmps[key][1], col))
         ops.small_attn_bwd(_dc(cd), N, H, Lq, Lk, E, go.data_ptr(), (so_l, so_n),
                            _ptr(q_src, qcol), (sq_l, sq_n), _ptr(k_src, kcol), (sk_l, sk_n),
                            _ptr(v_src, vcol), (sv_l, sv_n), P,
-                           _ptr(dq, qcol), (dq.stride(0), dq.stride(1)),
-                           _ptr(dk, kcol), (dk.stride(0), dk.stride(1)),
-                           _ptr(dv, vcol), (dv.stride(0), dv.stride(1)), scale)
+                           *[a for t, c in outs for a in (_ptr(t, c), (t.stride(0), t.stride(1)))],
+                           scale)
+        for buf, tmp in tmps.values():
+            buf.copy_(tmp)
         return
     bS = (H * Lq * ldS, Lq * ldS)
     dS = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
@@ -991,3 +1010,54 @@ def ccc_loss_ignore(pred, label, ignore=-5.0, group=None):
     # is the sum of the ranks' sizes (-1: summed on the device by jmt_ccc_finish)
     bs = pred.shape[0] if pred.dim() >= 2 else -1
     return CCCLossFn.apply(pred, label, 1, 1, float(ignore), -1.0, 1.0, 0.0, int(bs), group)
+
+
+class CELossFn(Function):
+    """losses/loss.py:34-51 CELoss on the device: digitize + weighted log-softmax NLL in one
+    statistics kernel, (optional) all-gather of 4 doubles per rank, one finish kernel; backward
+    one elementwise kernel.  No host synchronisation (the reference digitizes on the host)."""
+
+    @staticmethod
+    def forward(ctx, x, label, k, lo, hi, weights, group):
+        dev = x.device
+        xc = x if x.is_contiguous() else x.contiguous()
+        lab = label.reshape(-1)
+        if lab.dtype != torch.float32 or not lab.is_contiguous():
+            lab = ops.cast(lab, torch.float32)
+        w = None
+        if weights is not None:
+            w = weights.to(device=dev, dtype=torch.float32).contiguous()
+        stats = torch.empty(4, dtype=torch.float64, device=dev)
+        ops.ce_stats(xc, lab, k, lo, hi, w, stats)
+        world, stats_all = 1, stats
+        if group is not None:
+            import torch.distributed as dist
+            world = dist.get_world_size(group)
+            if world > 1:
+                stats_all = torch.empty(4 * world, dtype=torch.float64, device=dev)
+                dist.all_gather_into_tensor(stats_all, stats, group=group)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        coef = torch.empty(1, dtype=torch.float64, device=dev)
+        ops.ce_finish(world, stats_all, loss, coef)
+        ctx.save_for_backward(xc, lab, coef, w)
+        ctx.meta = (k, lo, hi, x.shape)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, lab, coef, w = ctx.saved_tensors
+        k, lo, hi, shape = ctx.meta
+        g = g.to(torch.float32).contiguous()
+        dx = torch.empty_like(x)
+        ops.ce_bwd(x, lab, k, lo, hi, w, coef, g, dx)
+        return dx.view(shape), None, None, None, None, None, None
+
+
+def ce_loss(x, label, digitize_num, rng=(-1.0, 1.0), weights=None, group=None):
+    k = int(digitize_num)
+    if x.dim() != 2 or x.shape[1] != k:
+        raise ValueError(f"CELoss: logits must be (N, {k}), got {tuple(x.shape)}")
+    if label.numel() != x.shape[0]:
+        raise ValueError(f"CELoss: {label.numel()} labels for {x.shape[0]} rows")
+    return CELossFn.apply(x, label, k, float(rng[0]), float(rng[1]), weights, group)
+

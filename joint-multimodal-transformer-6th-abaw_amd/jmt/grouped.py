@@ -379,23 +379,34 @@ class EncoderGroupFn(Function):
         def ln_bwd(x, r, dy, st, gamma, beta, dx, bias=None):
             """LayerNorm backward per group; with `bias` (the biases of the linears whose
             outputs r entered the residual sums) their gradients — the column sums of dx — are
-            reduced in the same launch pair.  Returns whether they were."""
+            reduced in the same launch pair.  Returns whether they were.
+            The fused bias sum reduces the fp32 dx before it is rounded to the compute dtype;
+            the fallback column sum (_bias_grad) reads the rounded dx — the same quantity, one
+            rounding apart.  The kernels take one accumulate flag for all their outputs, so when
+            any of the gradient buffers is missing (a frozen parameter) every output goes to a
+            scratch block and the present buffers accumulate it afterwards."""
             fused = bias is not None
             for g in range(G):
-                dgam = _grad_buffer(gamma[g])
-                dbet = _grad_buffer(beta[g])
-                dbias = _grad_buffer(bias[g]) if bias is not None else None
+                bufs = [_grad_buffer(gamma[g]), _grad_buffer(beta[g])]
+                if fused:
+                    bufs.append(_grad_buffer(bias[g]))
                 tmp = None
-                if dgam is None or dbet is None or (bias is not None and dbias is None):
-                    tmp = torch.empty(3, E, dtype=torch.float32, device=dev)
+                if any(b is None for b in bufs):
+                    tmp = torch.zeros(3, E, dtype=torch.float32, device=dev)
+                outs = bufs if tmp is None else [tmp[0], tmp[1], tmp[2]]
                 args = (x[g], E, r[g], E, dy[g], E, st[0, g * R:], st[1, g * R:], gamma[g], dx[g],
-                        E, dgam if dgam is not None else tmp[0],
-                        dbet if dbet is not None else tmp[1])
-                if fused and ops.layernorm_bwd_dsum(
-                        *args, dbias if dbias is not None else tmp[2], tmp is None, R, E) is not None:
+                        E, outs[0], outs[1])
+                done = fused and ops.layernorm_bwd_dsum(
+                    *args, outs[2] if tmp is None else tmp[2], tmp is None, R, E) is not None
+                if not done:
+                    ops.layernorm_bwd(*args, tmp is None, R, E)
+                if tmp is not None:
+                    for b, t in zip(bufs[:3 if done else 2], tmp):
+                        if b is not None:
+                            b.add_(t)
+                if done:
                     _grad_done(gamma[g], beta[g], bias[g])
                     continue
-                ops.layernorm_bwd(*args, tmp is None, R, E)
                 _grad_done(gamma[g], beta[g])
                 if fused:        # shape not covered by the fused form: this group's bias apart
                     _bias_grad(dx[g].view(R, E), E, R, E, bias[g], 0)

@@ -304,6 +304,31 @@ def ccc_finish(kind, world, stats_all, bs, eps, loss, coef):
               coef.data_ptr(), stream())
 
 
+def ce_stats(x, label, k, lo, hi, weights, stats):
+    n = x.numel() // k
+    _lib.call("jmt_ce_stats", dt(x), n, k, x.data_ptr(), label.data_ptr(), lo, hi,
+              weights.data_ptr() if weights is not None else None, stats.data_ptr(), stream())
+
+
+def ce_finish(world, stats_all, loss, coef):
+    _lib.call("jmt_ce_finish", world, stats_all.data_ptr(), loss.data_ptr(), coef.data_ptr(),
+              stream())
+
+
+def ce_bwd(x, label, k, lo, hi, weights, coef, grad_loss, dx):
+    n = x.numel() // k
+    _lib.call("jmt_ce_bwd", dt(x), n, k, x.data_ptr(), label.data_ptr(), lo, hi,
+              weights.data_ptr() if weights is not None else None, coef.data_ptr(),
+              grad_loss.data_ptr() if grad_loss is not None else None, dx.data_ptr(), stream())
+
+
+def ce_labels(label, k, lo, hi):
+    out = torch.empty(label.numel(), dtype=torch.int64, device=label.device)
+    _lib.call("jmt_ce_labels", label.numel(), k, label.data_ptr(), lo, hi, out.data_ptr(),
+              stream())
+    return out
+
+
 def ccc_bwd(kind, pred, label, k, ignore, lo, hi, coef, grad_loss, dpred):
     n = label.numel()
     _lib.call("jmt_ccc_bwd", kind, dt(pred), n, k, pred.data_ptr(), label.data_ptr(), ignore, lo,

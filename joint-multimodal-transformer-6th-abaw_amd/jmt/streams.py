@@ -100,7 +100,7 @@ def run_parallel(fns: Sequence[Callable[[], object]], device) -> list:
 # stream right after the output gradient is enqueued, so their blocks fill the CUs the chain's
 # launches leave idle (tile-quantised last rounds, epilogue bursts, latency-bound phases).
 _side: dict = {}
-_side_join = {"queued": False}
+_side_join = {"queued": None}    # graph task id whose end-of-backward join is queued
 
 
 def set_side_enabled(on: bool) -> None:
@@ -133,11 +133,16 @@ def run_side(fn: Callable[[], object], reads: Sequence[Optional[torch.Tensor]] =
     for t in reads:
         if isinstance(t, torch.Tensor) and t.is_cuda:
             t.record_stream(side)
-    if not _side_join["queued"]:
-        _side_join["queued"] = True
+    # one join per backward pass, keyed on autograd's graph task (a backward that raised
+    # before its final callbacks ran cannot leave a stale flag that skips later joins)
+    task = torch._C._current_graph_task_id()
+    if task < 0:                       # outside a backward: the caller joins (wait_side)
+        return out
+    if _side_join["queued"] != task:
+        _side_join["queued"] = task
 
         def _cb():
-            _side_join["queued"] = False
+            _side_join["queued"] = None
             cur = torch.cuda.current_stream()
             for st in _side.values():
                 if st.device == cur.device:

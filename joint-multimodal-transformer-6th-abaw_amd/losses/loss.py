@@ -29,23 +29,22 @@ class CCCLoss(nn.Module):
 
 
 class CELoss(nn.Module):
-    """loss.py:34-51: cross entropy against labels digitized into `digitize_num` bins.
-    (Off the training path of the shipped config; numpy digitize on the host as the reference.)"""
+    """loss.py:34-51: cross entropy against labels digitized into `digitize_num` bins
+    (np.digitize over linspace(range, digitize_num + 1), top bin clamped) — digitize, weighted
+    log-softmax NLL and its gradient in HIP kernels (jmt_ce_*), no host round trip.  A label
+    below range[0] makes the reference raise in F.cross_entropy; here the loss is NaN."""
 
     def __init__(self, digitize_num, range=[-1, 1], weights=None):
         super(CELoss, self).__init__()
         self.digitize_num = digitize_num
+        self.range = range
         self.weights = torch.Tensor(weights) if weights is not None else None
         assert self.digitize_num != 1
         self.edges = np.linspace(*range, num=self.digitize_num + 1)
 
     def forward(self, x, y):
-        y = y.view(-1)
-        y_dig = np.digitize(y.detach().cpu().numpy(), self.edges) - 1
-        y_dig[y_dig == self.digitize_num] = self.digitize_num - 1
-        yt = torch.as_tensor(y_dig, dtype=torch.long, device=x.device)
-        w = self.weights.to(x.device) if self.weights is not None else None
-        return torch.nn.functional.cross_entropy(x, yt, weight=w)
+        return F.ce_loss(x, y.view(-1), self.digitize_num, rng=self.range, weights=self.weights,
+                         group=jdist.loss_group())
 
 
 class CCC_CE_Loss(nn.Module):

@@ -54,42 +54,51 @@ GAINS = (("in_proj_weight", 4.0), ("out_layer1.weight", 3.0), ("final_layer.weig
          ("regressor.3.weight", 3.0), ("mm_transformer.fc.weight", 3.0))
 
 
-def gain(name: str) -> float:
-    for pat, g in GAINS:
+# Gains of the CONDITIONED cases (round 3, tests/golden/spec.py COND_CASES): x2 (x3 at T=300) on
+# the packed in_proj weights only.  The CCC-trained GAINS cases above are ill-conditioned in 16
+# bits — the reference's own fp32 gradients move by 8-20 % when its weights are rounded to bf16,
+# and its own CPU autocast path is 7-90 % off (profiles/r03_parity_conditioning.txt) — so the
+# tight 16-bit ceilings are asserted on these instead.
+GAINS_COND = (("in_proj_weight", 2.0),)
+GAINS_COND_T300 = (("in_proj_weight", 3.0),)
+
+
+def gain(name: str, gains=None) -> float:
+    for pat, g in (GAINS if gains is None else gains):
         if pat in name:
             return g
     return 1.0
 
 
-def param_value(name: str, shape) -> np.ndarray:
+def param_value(name: str, shape, gains=None) -> np.ndarray:
     """Deterministic value for a parameter of the given state_dict name and shape.
 
     * 2-D weights: U(-g/sqrt(fan_in), g/sqrt(fan_in)), fan_in = shape[1] (nn.Linear convention),
-      g = gain(name) (1 except the GAINS above).
+      g = gain(name, gains) (1 except the GAINS above, or the case's own `gains`).
     * LayerNorm weight ('layer_norm*.weight'): 1 + U(-0.1, 0.1) so the affine path is exercised.
     * any other 1-D tensor (biases, LN bias): U(-0.1, 0.1).
     """
     shape = tuple(int(s) for s in shape)
     if len(shape) == 2:
-        b = gain(name) / np.sqrt(shape[1])
+        b = gain(name, gains) / np.sqrt(shape[1])
         return uniform("w:" + name, shape, -b, b)
     if "layer_norm" in name and name.endswith("weight"):
         return (1.0 + uniform("w:" + name, shape, -0.1, 0.1)).astype(np.float32)
     return uniform("w:" + name, shape, -0.1, 0.1)
 
 
-def init_module_(module, prefix: str = "") -> None:
+def init_module_(module, prefix: str = "", gains=None) -> None:
     """Overwrite every parameter of a torch module in place with param_value(prefix+name)."""
     import torch
 
     with torch.no_grad():
         for name, p in module.named_parameters():
-            v = torch.from_numpy(param_value(prefix + name, p.shape))
+            v = torch.from_numpy(param_value(prefix + name, p.shape, gains))
             p.copy_(v.to(dtype=p.dtype, device=p.device))
 
 
-def state_dict_values(shapes: dict, prefix: str = "") -> dict:
-    return {k: param_value(prefix + k, s) for k, s in shapes.items()}
+def state_dict_values(shapes: dict, prefix: str = "", gains=None) -> dict:
+    return {k: param_value(prefix + k, s, gains) for k, s in shapes.items()}
 
 
 def features(tag: str, shape) -> np.ndarray:
@@ -104,3 +113,10 @@ def labels(tag: str, shape, ignore_frac: float = 0.0, ignore: float = -5.0) -> n
         m = uniform01("m:" + tag, y.size).reshape(y.shape) < ignore_frac
         y = np.where(m, np.float32(ignore), y).astype(np.float32)
     return y
+
+
+def proj_weights(tag: str, shape) -> np.ndarray:
+    """Per-element weights of the conditioned cases' loss, mean(w * prediction), in [0.5, 1.5]:
+    a smooth, non-cancelling objective (every window contributes with one sign), so each
+    parameter gradient is a well-conditioned sum (tests/golden/spec.py COND_CASES)."""
+    return (1.0 + 0.5 * features(tag, shape)).astype(np.float32)

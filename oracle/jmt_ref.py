@@ -453,6 +453,6 @@ def intra_modal_shapes(feat_dim: int, L: int, hidden_dim: int = 512) -> dict:
     return d
 
 
-def hash_params(shapes: dict, prefix: str = "") -> P:
+def hash_params(shapes: dict, prefix: str = "", gains=None) -> P:
     from oracle.hashinit import param_value
-    return {k: torch.from_numpy(param_value(prefix + k, s)) for k, s in shapes.items()}
+    return {k: torch.from_numpy(param_value(prefix + k, s, gains)) for k, s in shapes.items()}

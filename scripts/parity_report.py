@@ -1,6 +1,12 @@
-"""Parity report: HIP drop-in modules vs the reference goldens in fp32 / bf16 / fp16 compute.
-Prints one JSON line per (case, dtype) with every error the tests bound (tests/parity.py).
-Needs a GPU.  Usage: python scripts/parity_report.py [--full]"""
+"""Parity report (needs a GPU): every error the 16-bit tests bound, with its bound and margin.
+
+* strict suite (spec.COND_CASES, tests/parity.py check16_strict): per (case, dtype) the GPU error,
+  the rounding-emulating oracle's error and the bound min(ceiling, K_STRICT x emulated) of every
+  quantity; the line lists the smallest margins (bound / GPU error) and the GPU / emulated ratios.
+* reference-relative suite (spec.TT_CASES, check_vs_ref16): GPU vs the reference's own autocast
+  and the emulating oracle on prediction / loss / median and max parameter-gradient error.
+
+    python scripts/parity_report.py > gpurun_out/parity_report.jsonl"""
 import json
 import os
 import sys
@@ -12,20 +18,45 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from tests.golden import spec  # noqa: E402
-from tests.parity import measure  # noqa: E402
+from tests import parity as P  # noqa: E402
 
 
 def main():
-    full = "--full" in sys.argv
     with np.load(os.path.join(REPO, "tests", "golden", "golden.npz")) as z:
         gold = {k: z[k] for k in z.files}
+    for c in spec.COND_CASES:
+        for cd in (torch.bfloat16, torch.float16):
+            gpu = P.measure_strict(gold, c, cd)
+            emu = P.emulated_strict(gold, c, cd)
+            bnd = P.strict_bounds(emu, cd)
+            margin = {k: (bnd[k] / gpu[k] if gpu[k] > 0 else float("inf")) for k in gpu}
+            ratio = [gpu[k] / emu[k] for k in gpu if emu[k] > 0]
+            worst = sorted(margin, key=margin.get)[:5]
+            kinds = {}
+            for k in gpu:
+                kind = k.split(":")[0]
+                kinds.setdefault(kind, []).append(gpu[k])
+            print(json.dumps({
+                "suite": "strict", "case": c["tag"], "dtype": str(cd)[6:],
+                "n_quantities": len(gpu), "violations": len(P.check16_strict(gpu, emu, cd)),
+                "min_margin": round(margin[worst[0]], 3),
+                "worst": [{"q": k, "gpu": round(gpu[k], 6), "emulated": round(emu[k], 6),
+                           "bound": round(bnd[k], 6), "margin": round(margin[k], 3)}
+                          for k in worst],
+                "max_err_by_kind": {k: round(max(v), 6) for k, v in kinds.items()},
+                "gpu_over_emulated": {"median": round(float(np.median(ratio)), 3),
+                                      "p90": round(float(np.percentile(ratio, 90)), 3),
+                                      "max": round(float(max(ratio)), 3)}}), flush=True)
     for c in spec.TT_CASES:
-        for cd in (torch.float32, torch.bfloat16, torch.float16):
-            r = measure(gold, c, cd)
-            if not full:
-                r.pop("pgrad", None)
-                r.pop("inter", None)
-            print(json.dumps(r), flush=True)
+        for cd in (torch.bfloat16, torch.float16):
+            gpu = P.run_stats(P.measure(gold, c, cd))
+            emu = P.run_stats(P.emulated(gold, c, cd))
+            ref = P.ref16_stats(gold, c["tag"], cd)
+            print(json.dumps({
+                "suite": "vs_reference_autocast", "case": c["tag"], "dtype": str(cd)[6:],
+                "gpu": {k: round(v, 6) for k, v in gpu.items()},
+                "reference_autocast": {k: round(v, 6) for k, v in ref.items()},
+                "emulated": {k: round(v, 6) for k, v in emu.items()}}), flush=True)
 
 
 if __name__ == "__main__":

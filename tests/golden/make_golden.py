@@ -138,8 +138,8 @@ def run_two_transformers(mods, out, c):
     model = mods["models.two_transformers"].Two_transformers(
         0.0, 0.0, c["H"], c["L"], c["jm"], c["fmt"], c["vin"])
     fc = mods["models.fc_layer"].FcLayer(1024, 512)
-    hi.init_module_(model, "")
-    hi.init_module_(fc, "fc.")
+    hi.init_module_(model, "", c.get("gains"))
+    hi.init_module_(fc, "fc.", c.get("gains"))
     model.train()
     B, T = c["B"], c["T"]
     audio, video, lv, la = spec.tt_inputs(tag, B, T, c["vin"])
@@ -158,8 +158,13 @@ def run_two_transformers(mods, out, c):
     aout = ao.view(-1, ao.shape[0] * ao.shape[1])
     vt = torch.from_numpy(lv).view(-1, B * T)
     at = torch.from_numpy(la).view(-1, B * T)
-    l1 = crit(vout, vt)
-    l2 = crit(aout, at)
+    if c.get("loss") == "proj":          # conditioned cases: mean(w * outputs), spec.COND_CASES
+        wv, wa = (torch.from_numpy(w) for w in spec.proj_inputs(c))
+        l1 = (vo * wv).mean()
+        l2 = (ao * wa).mean()
+    else:
+        l1 = crit(vout, vt)
+        l2 = crit(aout, at)
     out[f"{tag}/v_loss"] = np.array(float(l1))
     out[f"{tag}/a_loss"] = np.array(float(l2))
     (l1 + l2).backward()
@@ -188,6 +193,56 @@ def run_two_transformers(mods, out, c):
         out[f"{tag}/train_losses"] = np.array(losses)
         out[f"{tag}/train_final_out_layer1_w_sample"] = (
             model.mm_transformer.out_layer1.weight.detach().reshape(-1)[:N_SAMPLE].numpy())
+
+
+def _tt_once(mods, c, ac_dtype):
+    """(vouts, aouts, v_loss, a_loss, {param: grad}) of one case through the reference, fp32 or
+    under CPU autocast in `ac_dtype` (the reference's own 16-bit path: train.py:101 runs the
+    model under autocast; fp16 under loss scaling 1024 as its GradScaler, train.py:89)."""
+    torch.manual_seed(0)
+    model = mods["models.two_transformers"].Two_transformers(
+        0.0, 0.0, c["H"], c["L"], c["jm"], c["fmt"], c["vin"])
+    fc = mods["models.fc_layer"].FcLayer(1024, 512)
+    hi.init_module_(model, "", c.get("gains"))
+    hi.init_module_(fc, "fc.", c.get("gains"))
+    B, T = c["B"], c["T"]
+    audio, video, lv, la = spec.tt_inputs(c["tag"], B, T, c["vin"])
+    crit = make_loss(mods, "CCCLoss", 1)
+    ctx = (torch.autocast("cpu", dtype=ac_dtype) if ac_dtype is not None
+           else torch.autocast("cpu", enabled=False))
+    with ctx:
+        vo, ao = model(fc(torch.from_numpy(audio)), torch.from_numpy(video))
+    vo, ao = vo.float(), ao.float()
+    if c.get("loss") == "proj":
+        wv, wa = (torch.from_numpy(w) for w in spec.proj_inputs(c))
+        l1, l2 = (vo * wv).mean(), (ao * wa).mean()
+    else:
+        l1 = crit(vo.reshape(1, -1), torch.from_numpy(lv).view(1, -1))
+        l2 = crit(ao.reshape(1, -1), torch.from_numpy(la).view(1, -1))
+    scale = 1024.0 if ac_dtype == torch.float16 else 1.0
+    ((l1 + l2) * scale).backward()
+    named = list(model.named_parameters()) + [("fc." + n, p) for n, p in fc.named_parameters()]
+    grads = {n: p.grad.detach().double() / scale for n, p in named if p.grad is not None}
+    return vo.detach().double(), ao.detach().double(), float(l1), float(l2), grads
+
+
+def ref16_errors(mods, out, c):
+    """The reference's OWN 16-bit error on the case: its CPU autocast bf16 / fp16 run vs its
+    fp32 run — prediction error over the prediction spread, loss error, and the relative L2
+    error of every parameter gradient (names in `{tag}/ref16_param_names`).  Context for the
+    16-bit tests: what the reference itself achieves in 16 bits on the same weights and inputs."""
+    tag = c["tag"]
+    rvo, rao, rl1, rl2, rg = _tt_once(mods, c, None)
+    names = sorted(rg)
+    out[f"{tag}/ref16_param_names"] = np.array(names)
+    for dt, key in ((torch.bfloat16, "bf16"), (torch.float16, "fp16")):
+        vo, ao, l1, l2, g = _tt_once(mods, c, dt)
+        spread = max(float(rvo.max() - rvo.min()), float(rao.max() - rao.min()), 1e-30)
+        out[f"{tag}/ref16_{key}/out_of_spread"] = np.array(
+            max(float((vo - rvo).abs().max()), float((ao - rao).abs().max())) / spread)
+        out[f"{tag}/ref16_{key}/loss_abs"] = np.array(max(abs(l1 - rl1), abs(l2 - rl2)))
+        out[f"{tag}/ref16_{key}/pgrad"] = np.array(
+            [float((g[n] - rg[n]).norm() / max(float(rg[n].norm()), 1e-30)) for n in names])
 
 
 def run_intra(mods, out, c):
@@ -237,9 +292,10 @@ def main():
     mods = import_reference()
     torch.set_num_threads(8)
     out = {}
-    for c in spec.TT_CASES:
+    for c in spec.ALL_TT_CASES:
         print("case", c["tag"], flush=True)
         run_two_transformers(mods, out, c)
+        ref16_errors(mods, out, c)
     for c in spec.INTRA_CASES:
         print("case", c["tag"], flush=True)
         run_intra(mods, out, c)

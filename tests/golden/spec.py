@@ -22,6 +22,41 @@ TT_CASES = [
     dict(tag="fcjoint", jm="FC", fmt="FC", H=1, L=1, B=3, T=37, vin=512),
 ]
 
+# Conditioned cases (round 3): the STRICT 16-bit suite (tests/parity.py check16_strict: every
+# error <= min(ceiling, K16 x the rounding-emulating oracle's), ceilings 5 % bf16 / 2 % fp16 on
+# predictions, losses and every parameter gradient).  Gains only on in_proj (oracle/hashinit.py
+# GAINS_COND: attention peaked enough to carry signal) and the objective
+# mean(w_v * vouts) + mean(w_a * aouts) with w in [0.5, 1.5] (hashinit.proj_weights): each
+# parameter gradient is then a well-conditioned sum.  The CCC-trained GAINS cases above are kept
+# for fp32 and for the comparison with the reference's own 16-bit autocast path.
+COND_CASES = [
+    dict(tag="cond_tr_fc", jm="TRANSFORMER", fmt="FC", H=1, L=1, B=4, T=61, vin=2048,
+         inter=True, gains=hi.GAINS_COND, loss="proj"),
+    dict(tag="cond_tr_fc_t300", jm="TRANSFORMER", fmt="FC", H=1, L=1, B=2, T=300, vin=2048,
+         inter=True, gains=hi.GAINS_COND_T300, loss="proj"),
+    dict(tag="cond_none_fc", jm="NONE", fmt="FC", H=1, L=1, B=8, T=37, vin=2048, inter=True,
+         gains=hi.GAINS_COND, loss="proj"),
+    dict(tag="cond_tr_sa", jm="TRANSFORMER", fmt="SELF_ATTEN", H=1, L=1, B=2, T=37, vin=2048,
+         inter=True, gains=hi.GAINS_COND, loss="proj"),
+    dict(tag="cond_tr_fc_h8l2", jm="TRANSFORMER", fmt="FC", H=8, L=2, B=2, T=37, vin=2048,
+         gains=hi.GAINS_COND, loss="proj"),
+    dict(tag="cond_fcjoint", jm="FC", fmt="FC", H=1, L=1, B=8, T=61, vin=512,
+         gains=hi.GAINS_COND, loss="proj"),
+]
+ALL_TT_CASES = TT_CASES + COND_CASES
+
+
+def out_shape(c: dict):
+    """Shape of each regressor output: (T, B) for TRANSFORMER/FC (seq-first), else (B, T)."""
+    return (c["T"], c["B"]) if c["jm"] == "TRANSFORMER" and c["fmt"] == "FC" else (c["B"], c["T"])
+
+
+def proj_inputs(c: dict):
+    """(w_v, w_a) of a conditioned case's objective, shaped like the outputs."""
+    return (hi.proj_weights(c["tag"] + ".wv", out_shape(c)),
+            hi.proj_weights(c["tag"] + ".wa", out_shape(c)))
+
+
 # Intra_modal_transformer_fusion cases: config 1 exactly (B=2,T=64,D=512), plus the 768 path.
 INTRA_CASES = [
     dict(tag="intra", H=1, L=1, B=2, T=64, Da=512, Db=512),

@@ -31,11 +31,23 @@ def oracle_tt(c: dict, emulate=None, loss_scale: float = 1.0) -> dict:
         return _oracle_tt(c, loss_scale)
 
 
+def case_losses(c: dict, vo, ao, lv, la, ccc):
+    """The two losses of a golden case: train.py:303-311's CCC on the (1, B*T) views, or the
+    conditioned cases' mean(w * outputs) (spec.COND_CASES)."""
+    if c.get("loss") == "proj":
+        wv, wa = (torch.from_numpy(w).to(vo.device) for w in spec.proj_inputs(c))
+        return (vo.float() * wv).mean(), (ao.float() * wa).mean()
+    n = vo.shape[0] * vo.shape[1]
+    return (ccc(vo.reshape(1, n), lv.reshape(1, n).to(vo.device)),
+            ccc(ao.reshape(1, n), la.reshape(1, n).to(ao.device)))
+
+
 def _oracle_tt(c: dict, loss_scale: float) -> dict:
     tag = c["tag"]
     shapes = R.two_transformers_shapes(c["L"], c["jm"], c["fmt"], c["vin"])
-    p = R.hash_params(shapes, "")
-    fcp = R.hash_params({"fc_layer.weight": (512, 1024), "fc_layer.bias": (512,)}, "fc.")
+    p = R.hash_params(shapes, "", c.get("gains"))
+    fcp = R.hash_params({"fc_layer.weight": (512, 1024), "fc_layer.bias": (512,)}, "fc.",
+                        c.get("gains"))
     B, T = c["B"], c["T"]
     audio, video, lv, la = spec.tt_inputs(tag, B, T, c["vin"])
     for t in list(p.values()) + list(fcp.values()):
@@ -48,8 +60,7 @@ def _oracle_tt(c: dict, loss_scale: float) -> dict:
                                         taps=taps)
     for t, _ in taps.values():
         t.retain_grad()
-    l1 = R.ccc_loss(vo.reshape(1, -1), torch.from_numpy(lv).reshape(1, -1))
-    l2 = R.ccc_loss(ao.reshape(1, -1), torch.from_numpy(la).reshape(1, -1))
+    l1, l2 = case_losses(c, vo, ao, torch.from_numpy(lv), torch.from_numpy(la), R.ccc_loss)
     ((l1 + l2) * loss_scale).backward()
     uns = lambda g: None if g is None else g / loss_scale
     res = {"vouts": vo.detach().numpy(), "aouts": ao.detach().numpy(),

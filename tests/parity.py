@@ -23,8 +23,8 @@ def build_tt(c):
     from models.fc_layer import FcLayer
     m = Two_transformers(0.0, 0.0, c["H"], c["L"], c["jm"], c["fmt"], c["vin"])
     fc = FcLayer(1024, 512)
-    init_module_(m, "")
-    init_module_(fc, "fc.")
+    init_module_(m, "", c.get("gains"))
+    init_module_(fc, "fc.", c.get("gains"))
     return m.to(DEV), fc.to(DEV)
 
 
@@ -37,6 +37,7 @@ def run_tt(c, cd, record=False, loss_scale: float = 1.0, model=None):
     audio, video, lv, la = spec.tt_inputs(c["tag"], B, T, c["vin"])
     a = torch.from_numpy(audio).to(DEV).requires_grad_(True)
     v = torch.from_numpy(video).to(DEV).requires_grad_(True)
+    from tests.oracle_cases import case_losses
     crit = CCCLoss(1)
     store = {}
     if record:
@@ -44,10 +45,7 @@ def run_tt(c, cd, record=False, loss_scale: float = 1.0, model=None):
     try:
         with JF.compute_mode(cd):
             vo, ao = m(fc(a), v)
-            vout = vo.view(-1, vo.shape[0] * vo.shape[1])
-            aout = ao.view(-1, ao.shape[0] * ao.shape[1])
-            l1 = crit(vout, torch.from_numpy(lv).to(DEV).view(-1, B * T))
-            l2 = crit(aout, torch.from_numpy(la).to(DEV).view(-1, B * T))
+            l1, l2 = case_losses(c, vo, ao, torch.from_numpy(lv), torch.from_numpy(la), crit)
             ((l1 + l2) * loss_scale).backward()
     finally:
         taps.disable()
@@ -131,51 +129,97 @@ def emulated(golden: dict, c: dict, cd) -> dict:
                   o["taps"])
 
 
-# 16-bit error model (tests/test_gpu_models.py): every error of the HIP run must stay within
-# K16 x the error of the rounding-emulating oracle on the same case, with floors: u = 2^-8 (bf16)
-# / 2^-11 (fp16) unit roundoff of 16-bit storage, and — because a single quantity's emulated error
-# can be small by luck of cancellation while its neighbours' is not — the largest emulated error
-# of its group: intermediates by (kind of tap, value/gradient), parameter gradients by layer.
-# Measured GPU / emulated ratios (profiles/r02_parity_error_model.txt): median 1.0, p99 ~3.
-K16 = 4.0
-UNIT = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11}
+# ---- STRICT 16-bit suite (round 3; spec.COND_CASES, tests/test_gpu_models.py) ----------------
+# bound(q) = min(CEIL[kind], K_STRICT x max(emulated error of q, 2u)): the HIP run may be at most
+# K_STRICT times as far from the fp32 reference as the rounding-emulating oracle on the SAME
+# quantity (no group / median floors), and never beyond an absolute ceiling: 5 % (bf16) / 2 %
+# (fp16) relative on predictions, losses and every parameter gradient; 8 % / 3 % on the recorded
+# intermediates and their gradients (8 sampled rows each).  Margins (bound / error) of every
+# quantity are reported by scripts/parity_report.py (profiles/r03_parity_error_model.txt).
+UNIT = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11}   # unit roundoff of 16-bit storage
+K_STRICT = 3.0
+CEIL = {torch.bfloat16: {"param": 0.05, "out": 0.05, "inter": 0.08},
+        torch.float16: {"param": 0.02, "out": 0.02, "inter": 0.03}}
 
 
-def _inter_group(k: str) -> str:
-    name, kind = k.split(":")
-    return name.split(".")[0] + ":" + kind
+def strict_errors(golden: dict, c: dict, vo, ao, l1, l2, grads, store) -> dict:
+    """{quantity: relative error} of one run of a conditioned case: predictions (max-abs relative
+    to the largest |prediction|), the two losses (relative), every parameter / input gradient
+    (grad_errors), every recorded intermediate and its gradient (inter_errors)."""
+    tag = c["tag"]
+    q = {}
+    for k, o in (("vouts", vo), ("aouts", ao)):
+        a = np.asarray(o.detach().float().cpu().numpy() if torch.is_tensor(o) else o, np.float64)
+        b = golden[f"{tag}/{k}"].astype(np.float64)
+        q["out:" + k] = float(np.abs(a - b).max() / np.abs(b).max())
+    for k, l in (("v_loss", l1), ("a_loss", l2)):
+        ref = float(golden[f"{tag}/{k}"])
+        q["out:" + k] = abs(float(l) - ref) / abs(ref)
+    for k, e in grad_errors(golden, tag, grads).items():
+        q["param:" + k] = e
+    if c.get("inter"):
+        for k, e in inter_errors(golden, tag, store).items():
+            q["inter:" + k] = e
+    return q
 
 
-def _param_group(k: str) -> str:
-    parts = k.split(".")
-    if "layers" in parts:
-        return ".".join(parts[:parts.index("layers") + 2])
-    return ".".join(parts[:-1]) or k
+def measure_strict(golden: dict, c: dict, cd, model=None) -> dict:
+    res = run_tt(c, cd, record=bool(c.get("inter")), loss_scale=LOSS_SCALE[cd], model=model)
+    return strict_errors(golden, c, *res)
 
 
-def check16(gpu: dict, emu: dict, cd) -> list:
-    """-> list of (quantity, gpu_err, bound) that break the error model."""
+def emulated_strict(golden: dict, c: dict, cd) -> dict:
+    from tests.oracle_cases import oracle_tt
+    torch.set_num_threads(min(16, max(1, len(os.sched_getaffinity(0)))))
+    o = oracle_tt(c, cd, LOSS_SCALE[cd])
+    return strict_errors(golden, c, o["vouts"], o["aouts"], o["v_loss"], o["a_loss"], o["grads"],
+                         o["taps"])
+
+
+def strict_bounds(emu: dict, cd) -> dict:
     u = UNIT[cd]
+    return {k: min(CEIL[cd][k.split(":")[0]], K_STRICT * max(e, 2 * u)) for k, e in emu.items()}
+
+
+def check16_strict(gpu: dict, emu: dict, cd) -> list:
+    """-> list of (quantity, gpu_err, bound) breaking the strict bounds (a zero reference
+    gradient — an unused parameter — must be exactly zero: grad_errors gives 0 or inf)."""
+    b = strict_bounds(emu, cd)
+    return [(k, gpu[k], b[k]) for k in emu if not (gpu[k] <= b[k])]
+
+
+# ---- comparison with the reference's own 16-bit path (spec.TT_CASES) -------------------------
+# The CCC-trained golden cases are ill-conditioned in 16 bits: the reference's own fp32 gradients
+# move by up to 20 % when only its weights are rounded to bf16, and its own CPU autocast run
+# (golden `{tag}/ref16_{bf16,fp16}/*`, make_golden.py ref16_errors) is 7-90 % off in bf16
+# (profiles/r03_parity_conditioning.txt).  No 16-bit tolerance below that is meaningful there, so
+# those cases assert that the HIP path is NOT LESS ACCURATE than the reference's own 16-bit path:
+# prediction / loss errors and the median and maximum parameter-gradient error each within
+# REF16_SLACK x max(the reference autocast's, the emulating oracle's) of the same statistic.
+REF16_SLACK = 1.5
+
+
+def ref16_stats(golden: dict, tag: str, cd) -> dict:
+    key = "bf16" if cd == torch.bfloat16 else "fp16"
+    pg = golden[f"{tag}/ref16_{key}/pgrad"]
+    return {"out_of_spread": float(golden[f"{tag}/ref16_{key}/out_of_spread"]),
+            "loss_abs": float(golden[f"{tag}/ref16_{key}/loss_abs"]),
+            "pgrad_median": float(np.median(pg)), "pgrad_max": float(pg.max())}
+
+
+def run_stats(r: dict) -> dict:
+    pg = [v for v in r["pgrad"].values() if np.isfinite(v)]
+    return {"out_of_spread": max(r["vouts_of_spread"], r["aouts_of_spread"]),
+            "loss_abs": r["loss_abs"], "pgrad_median": float(np.median(pg)),
+            "pgrad_max": float(max(pg)) if all(np.isfinite(v) for v in r["pgrad"].values())
+            else float("inf")}
+
+
+def check_vs_ref16(golden: dict, tag: str, gpu: dict, emu: dict, cd) -> list:
+    ref, g, e = ref16_stats(golden, tag, cd), run_stats(gpu), run_stats(emu)
     bad = []
-
-    def chk(name, g, e, floor):
-        bound = K16 * max(e, floor)
-        if not (g <= bound):
-            bad.append((name, g, bound))
-
-    for k in ("vouts_of_spread", "aouts_of_spread"):
-        chk(k, gpu[k], emu[k], u)
-    chk("loss_abs", gpu["loss_abs"], emu["loss_abs"], u)
-    if "inter" in gpu:
-        gmax = {}
-        for k, e in emu["inter"].items():
-            gmax[_inter_group(k)] = max(gmax.get(_inter_group(k), 0.0), e)
-        for k, g in gpu["inter"].items():
-            chk("inter:" + k, g, emu["inter"][k], max(2 * u, gmax[_inter_group(k)]))
-    med = float(np.median(list(emu["pgrad"].values())))
-    pmax = {}
-    for k, e in emu["pgrad"].items():
-        pmax[_param_group(k)] = max(pmax.get(_param_group(k), 0.0), e)
-    for k, g in gpu["pgrad"].items():
-        chk("pgrad:" + k, g, emu["pgrad"][k], max(med, 2 * u, pmax[_param_group(k)]))
+    for k in ref:
+        bound = REF16_SLACK * max(ref[k], e[k], 2 * UNIT[cd] if k != "loss_abs" else 0.0)
+        if not (g[k] <= bound):
+            bad.append((k, g[k], bound))
     return bad

@@ -15,7 +15,7 @@ import torch
 from jmt import functional as JF
 from oracle import jmt_ref as R
 from oracle.hashinit import init_module_
-from tests.parity import K16, UNIT
+from tests.parity import CEIL, K_STRICT, UNIT
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
@@ -46,35 +46,94 @@ def _oracle_fwd(p, fp, audio, video, jm, vin):
         return R.two_transformers_forward(aud, video, p, 1, 1, jm, "FC", vin)
 
 
-def test_c3_bench_shape_window_subset_bf16():
+def _rel(a, b) -> float:
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def test_c3_bench_shape_window_subset_bf16_strict():
+    """configs[2] at the bench shape (B=64, T=300) in bf16 with the conditioned hash-init
+    weights (oracle/hashinit.py GAINS_COND_T300): the GPU runs the WHOLE batch; the objective
+    weights (hashinit.proj_weights) are zero outside windows {0, 21, 42, 63}, so every gradient
+    is exactly those windows' (attention is per window in TRANSFORMER mode) and the fp32 oracle
+    on the 4 windows is the reference.  Predictions and EVERY parameter gradient (out_layer1,
+    in_proj, encoders, regressors, ...) within the strict 16-bit bound (tests/parity.py:
+    min(5 %, K_STRICT x the rounding-emulating oracle's error)).  The full-batch CCC losses of the
+    GPU predictions are checked against the oracle's CCC of the same predictions."""
     from losses.loss import CCCLoss
+    from oracle.hashinit import GAINS_COND_T300, features, labels, proj_weights
+    from tests.parity import CEIL, K_STRICT, UNIT, build_tt
     torch.set_num_threads(16)
-    B, T = 64, 300
-    m, fc = _models("TRANSFORMER", 2048, T, hashed=False)
-    g = torch.Generator(device=DEV).manual_seed(1000)
-    audio = torch.randn(B, T, 1024, device=DEV, generator=g)
-    video = torch.randn(B, T, 2048, device=DEV, generator=g)
-    lv = (torch.rand(B, T, device=DEV, generator=g) * 2 - 1).view(-1, B * T)
-    la = (torch.rand(B, T, device=DEV, generator=g) * 2 - 1).view(-1, B * T)
-    crit = CCCLoss(1)
-    with JF.compute_mode(torch.bfloat16):
-        vo, ao = m(fc(audio), video)                         # (T, B) seq-first, as the reference
-        l1 = crit(vo.view(-1, B * T), lv)
-        l2 = crit(ao.view(-1, B * T), la)
-        (l1 + l2).backward()
-    torch.cuda.synchronize()
-    p, fp = _state(m, fc)
+    B, T, cd = 64, 300, torch.bfloat16
     win = [0, 21, 42, 63]
-    rvo, rao = _oracle_fwd(p, fp, audio[win].cpu(), video[win].cpu(), "TRANSFORMER", 2048)
-    for got, ref in ((vo[:, win], rvo), (ao[:, win], rao)):
-        err = float((got.float().cpu() - ref).abs().max())
-        assert err <= 1e-2, err                              # north_star bf16 bound
-    # full-batch losses: the GPU CCC of the GPU predictions == the oracle CCC of them (fp32)
-    rl1 = float(R.ccc_loss(vo.detach().float().cpu().reshape(1, -1), lv.cpu()))
-    rl2 = float(R.ccc_loss(ao.detach().float().cpu().reshape(1, -1), la.cpu()))
+    c = dict(tag="c3b", jm="TRANSFORMER", fmt="FC", H=1, L=1, B=B, T=T, vin=2048,
+             gains=GAINS_COND_T300)
+    m, fc = build_tt(c)
+    audio = torch.from_numpy(features("c3b.audio", (B, T, 1024)))
+    video = torch.from_numpy(features("c3b.video", (B, T, 2048)))
+    lv = torch.from_numpy(labels("c3b.lv", (B, T)))
+    la = torch.from_numpy(labels("c3b.la", (B, T)))
+    wsub = [torch.from_numpy(proj_weights(f"c3b.w{k}", (T, len(win)))) for k in "va"]
+    wfull = [torch.zeros(T, B) for _ in range(2)]
+    for wf, ws in zip(wfull, wsub):
+        wf[:, win] = ws
+    n = float(T * len(win))
+    crit = CCCLoss(1)
+    with JF.compute_mode(cd):
+        vo, ao = m(fc(audio.to(DEV)), video.to(DEV))          # (T, B) seq-first
+        obj = (vo.float() * wfull[0].to(DEV)).sum() / n + (ao.float() * wfull[1].to(DEV)).sum() / n
+        obj.backward()
+        with torch.no_grad():
+            l1 = crit(vo.reshape(1, -1), lv.to(DEV).view(1, -1))
+            l2 = crit(ao.reshape(1, -1), la.to(DEV).view(1, -1))
+    torch.cuda.synchronize()
+    gpu = {k: p.grad.detach().float().cpu() for k, p in m.named_parameters() if p.grad is not None}
+    gpu.update({"fc." + k: p.grad.detach().float().cpu() for k, p in fc.named_parameters()})
+    # full-batch CCC of the GPU predictions: the CCC kernels vs the oracle's formula
+    rl1 = float(R.ccc_loss(vo.detach().float().cpu().reshape(1, -1), lv.reshape(1, -1)))
+    rl2 = float(R.ccc_loss(ao.detach().float().cpu().reshape(1, -1), la.reshape(1, -1)))
     assert abs(float(l1) - rl1) <= 1e-5 and abs(float(l2) - rl2) <= 1e-5, (float(l1), rl1)
-    gw = m.mm_transformer.out_layer1.weight.grad
-    assert gw is not None and bool(torch.isfinite(gw).all()) and float(gw.abs().max()) > 0
+
+    p0 = {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
+    fp0 = {k: v.detach().float().cpu() for k, v in fc.state_dict().items()}
+
+    def oracle(emulate):
+        import contextlib
+        pp = {k: t.clone().requires_grad_(True) for k, t in p0.items()}
+        fpp = {k: t.clone().requires_grad_(True) for k, t in fp0.items()}
+        with (R.emulate_storage(emulate) if emulate else contextlib.nullcontext()):
+            aud = R.linear(audio[win], fpp["fc_layer.weight"], fpp["fc_layer.bias"])
+            rvo, rao = R.two_transformers_forward(aud, video[win], pp, 1, 1, "TRANSFORMER", "FC",
+                                                  2048)
+            ((rvo * wsub[0]).sum() / n + (rao * wsub[1]).sum() / n).backward()
+        g = {k: t.grad for k, t in pp.items() if t.grad is not None}
+        g.update({"fc." + k: t.grad for k, t in fpp.items()})
+        return rvo.detach(), rao.detach(), g
+
+    rvo, rao, rg = oracle(None)
+    evo, eao, eg = oracle(cd)
+    assert set(gpu) >= set(rg), set(rg) - set(gpu)
+    u = UNIT[cd]
+
+    def bound(kind, e_emu):
+        return min(CEIL[cd][kind], K_STRICT * max(e_emu, 2 * u))
+
+    bad = []
+    mx = float(max(rvo.abs().max(), rao.abs().max()))
+    for name, got, emu, ref in (("vouts", vo.detach().float().cpu()[:, win], evo, rvo),
+                                ("aouts", ao.detach().float().cpu()[:, win], eao, rao)):
+        e_gpu = float((got - ref).abs().max()) / mx
+        e_emu = float((emu - ref).abs().max()) / mx
+        if not e_gpu <= bound("out", e_emu):
+            bad.append((name, e_gpu, bound("out", e_emu)))
+    for k in rg:
+        e_gpu, e_emu = _rel(gpu[k], rg[k]), _rel(eg[k], rg[k])
+        if not e_gpu <= bound("param", e_emu):
+            bad.append((k, e_gpu, bound("param", e_emu)))
+    for k in gpu:                                 # unused parameters (final_encoder): no grad
+        if k not in rg:
+            assert float(gpu[k].abs().max()) == 0.0, k
+    assert not bad, bad[:6]
 
 
 def _run_gpu(m, fc, audio, video, lv, la, cd):
@@ -122,11 +181,15 @@ def test_config_shapes_vs_oracle(cfg, cd):
         return
     with R.emulate_storage(cd):
         evo, eao, eloss = _oracle_loss(p, fp, audio, video, lv, la, jm, 2048)
+    # strict 16-bit bound (tests/parity.py): errors relative to the largest |prediction| / the
+    # loss, within min(5 %, K_STRICT x the rounding-emulating oracle's)
+    mx = float(max(rvo.abs().max(), rao.abs().max()))
     for got, emu, ref in ((vo, evo, rvo), (ao, eao, rao)):
-        e_gpu = float((got - ref).abs().max())
-        e_emu = float((emu - ref).abs().max())
-        assert e_gpu <= K16 * max(e_emu, UNIT[cd] * spread), (e_gpu, e_emu)
-    assert abs(loss - rloss) <= K16 * max(abs(eloss - rloss), UNIT[cd]), (loss, rloss, eloss)
+        e_gpu = float((got - ref).abs().max()) / mx
+        e_emu = float((emu - ref).abs().max()) / mx
+        assert e_gpu <= min(CEIL[cd]["out"], K_STRICT * max(e_emu, 2 * UNIT[cd])), (e_gpu, e_emu)
+    e_gpu, e_emu = abs(loss - rloss) / abs(rloss), abs(eloss - rloss) / abs(rloss)
+    assert e_gpu <= min(CEIL[cd]["out"], K_STRICT * max(e_emu, 2 * UNIT[cd])), (loss, rloss, eloss)
 
 
 def test_c5_expression_head_fp16_vs_oracle():
@@ -176,13 +239,15 @@ def test_c5_expression_head_fp16_vs_oracle():
     evo, eao, el, eg = oracle(True)
     spread = float(max(rvo.max() - rvo.min(), rao.max() - rao.min()))
     assert spread > 0.1, spread
+    bnd = lambda kind, e: min(CEIL[cd][kind], K_STRICT * max(e, 2 * UNIT[cd]))
+    mx = float(max(rvo.abs().max(), rao.abs().max()))
     for got, emu, ref in ((vo.detach().float().cpu(), evo, rvo), (ao.detach().float().cpu(), eao, rao)):
-        e_gpu = float((got - ref).abs().max())
-        e_emu = float((emu - ref).abs().max())
-        assert e_gpu <= K16 * max(e_emu, UNIT[cd] * spread), (e_gpu, e_emu)
-    assert abs(float(loss) - rl) <= K16 * max(abs(el - rl), UNIT[cd]), (float(loss), rl, el)
+        e_gpu = float((got - ref).abs().max()) / mx
+        e_emu = float((emu - ref).abs().max()) / mx
+        assert e_gpu <= bnd("out", e_emu), (e_gpu, e_emu)
+    assert abs(float(loss) - rl) / abs(rl) <= bnd("out", abs(el - rl) / abs(rl)), (float(loss), rl, el)
     for n in names:
         nrm = float(rg[n].norm())
         e_gpu = float((gpu_g[n] - rg[n]).norm()) / nrm
         e_emu = float((eg[n] - rg[n]).norm()) / nrm
-        assert e_gpu <= K16 * max(e_emu, 2 * UNIT[cd]), (n, e_gpu, e_emu)
+        assert e_gpu <= bnd("param", e_emu), (n, e_gpu, e_emu)

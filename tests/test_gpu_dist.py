@@ -304,3 +304,100 @@ def _spawn_raw(target, world=2):
     for p in procs:
         assert p.exitcode == 0, p.exitcode
     return out
+
+
+def _rccl1_worker(rank, world, port, q, mode):
+    """One rank with the nccl (RCCL) backend and the bucketer's collectives forced on at world
+    size 1 (GradBucketer.world1): the real RCCL launch path of bench.py's N>1 step on a 1-GPU box.
+    mode 'sync': one bucketed step under torch.cuda.set_sync_debug_mode('error') — the step
+    (forward, backward, bucket gating, all-reduces, fused SGD) must not synchronise the device.
+    mode 'graph': the same step captured into a hipGraph with the RCCL all-reduces inside
+    (bench.py's N>1 default), replayed; its parameters must equal eager steps' bit for bit."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", 0))
+    try:
+        from jmt import dist as jdist
+        from jmt import functional as JF
+        from jmt.graph import GraphedStep
+        from jmt.optim import FusedSGD
+        from losses.loss import CCCLoss
+        jdist.set_loss_group(dist.group.WORLD)
+        audio, video, lv, la = _inputs()
+        m = _model(hashed=False).cuda()
+        crit = CCCLoss(1)
+        a, v = audio.cuda(), video.cuda()
+        n = B * T
+        yv, ya = lv.cuda().view(-1, n), la.cuda().view(-1, n)
+
+        def fwd_bwd():
+            with JF.compute_mode(torch.bfloat16):
+                vo, ao = m(a, v)
+                loss = crit(vo.view(-1, n), yv) + crit(ao.view(-1, n), ya)
+                loss.backward()
+            return loss
+
+        params, counts = jdist.grad_write_profile(fwd_bwd, list(m.parameters()))
+        opt = FusedSGD(params, lr=1e-3, momentum=0.9, weight_decay=1e-4, nesterov=True,
+                       shadow_dtype=torch.bfloat16)
+        bk = jdist.GradBucketer(opt, counts, bucket_bytes=1 << 20, group=dist.group.WORLD)
+        bk.world1 = True
+
+        def step():
+            opt.zero_grad()
+            bk.begin()
+            loss = fwd_bwd()
+            bk.finish()
+            opt.step()
+            return loss
+
+        for _ in range(2):                              # first-step branches, allocator warm
+            step()
+        torch.cuda.synchronize()
+        if mode == "sync":
+            torch.cuda.set_sync_debug_mode("error")
+            try:
+                step()
+            finally:
+                torch.cuda.set_sync_debug_mode(0)
+            torch.cuda.synchronize()
+            q.put((rank, len(bk.buckets), len(bk.launch_log), None))
+        else:
+            bufs = [t for t in (opt.flat_p, opt.buf, opt.shadow) if t is not None]
+            snap = [t.clone() for t in bufs]
+
+            def rewind():
+                with torch.no_grad():
+                    for t, s in zip(bufs, snap):
+                        t.copy_(s)
+
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            eager = opt.flat_p.clone()
+            rewind()
+            g = GraphedStep(step).capture(warmup=1)
+            rewind()
+            for _ in range(3):
+                g.replay()
+            torch.cuda.synchronize()
+            same = bool(torch.equal(opt.flat_p, eager))
+            q.put((rank, len(bk.buckets), len(bk.launch_log), same))
+        bk.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["sync", "graph"])
+def test_rccl_bucketed_step_sync_free_and_capturable(mode):
+    """a bucketed step issues no device synchronisation, and the N>1 step
+    (RCCL all-reduces on the communication stream, gated per bucket) captures into a hipGraph
+    whose replay matches eager steps exactly."""
+    out = _spawn(_rccl1_worker, (mode,), world=1)
+    (_, nb, launched, same), = out
+    assert nb > 2 and launched == nb, (nb, launched)
+    if mode == "graph":
+        assert same
