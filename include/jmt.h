@@ -32,6 +32,10 @@ int jmt_abi_version(void);
 const char* jmt_last_error(void);
 /* number of gfx950 code objects / kernels compiled in (sanity probe, no GPU needed) */
 int jmt_kernel_count(void);
+/* Bounds-check build (csrc `make bounds`, -DJMT_BOUNDS=1, loaded with JMT_LIB=<path>): the
+ * number of failed device-side index checks since the last reset (reset != 0 clears them; the
+ * call synchronises the device); -1 in the default build, which compiles the checks out. */
+long long jmt_bounds_violations(int reset);
 
 /* ------------------------------------------------------------------ GEMM
  * C[b] = epilogue(alpha * A[b] . B[b]),  A: M x K, B: K x N, C: M x N.

@@ -91,6 +91,7 @@ __device__ __forceinline__ void stage_rows(char* img, const T* base, int64_t ld,
   for (int i = 0; i < NI; ++i) {
     const int r = wu * NI + i;
     const int src = min(k0 + r, Lk - 1);
+    JMT_DCHECK(src >= 0 && src < Lk);
     const char* row = (const char*)(base + (int64_t)src * ld);
     const unsigned off = (unsigned)(lane ^ ((r & 7) << 1)) << 4;
     glds16(row + off, img + r * AT_ROWB);
@@ -364,6 +365,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
     float lt = l_run;
     lt += __shfl_xor(lt, 16, 64);
     lt += __shfl_xor(lt, 32, 64);
+    JMT_DCHECK(item < p.nitems && n * p.H + hd == nh);
     if (qr < p.Lq && g == 0 && h == 0 && p.lse)
       p.lse[(int64_t)nh * p.Lq + qr] = (m_run + __builtin_amdgcn_logf(lt)) * 0.69314718055994531f;
     store_acc_direct<T>(o, 1.f / lt,
@@ -570,6 +572,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
           dsf[kt * 4 + r] = ds4[r];
         }
         const int key = kbase + 16 * kt;
+        JMT_DCHECK(qc >= 0 && qc < p.Lq && item < p.nitems);
         if (qr < p.Lq && key < p.ldp) {
           if (h == 0) *(uint2*)(prow_p + key) = *(const uint2*)pv4;
           else *(uint2*)(prow_ds + key) = *(const uint2*)ds4;

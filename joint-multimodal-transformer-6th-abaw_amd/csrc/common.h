@@ -34,6 +34,34 @@ int set_error(int code, const char* fmt, ...);
                               hipGetErrorString(e_));                                \
   } while (0)
 
+// ------------------------------------------------------------------ bounds-check build
+// `make bounds` compiles the kernels with -DJMT_BOUNDS=1: JMT_DCHECK(cond) at the kernels' global
+// index computations counts every failed check in a per-translation-unit device counter (a
+// vector atomic — never a trap, so a bad index is reported, not turned into a GPU fault) that
+// jmt_bounds_violations() (abi.cpp) sums over the library.  The default build compiles it out.
+int register_bounds_counter(unsigned (*read)(bool reset));
+#if defined(JMT_BOUNDS) && JMT_BOUNDS
+static __device__ unsigned g_jmt_bounds_hits;
+#define JMT_DCHECK(cond)                                                             \
+  do {                                                                               \
+    if (!(cond)) atomicAdd(&g_jmt_bounds_hits, 1u);                                  \
+  } while (0)
+static unsigned jmt_read_bounds_hits(bool reset) {
+  unsigned v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_jmt_bounds_hits), sizeof(v)) != hipSuccess) return 0;
+  if (reset) {
+    const unsigned z = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_jmt_bounds_hits), &z, sizeof(z));
+  }
+  return v;
+}
+static const int g_jmt_bounds_reg = register_bounds_counter(&jmt_read_bounds_hits);
+#else
+#define JMT_DCHECK(cond) \
+  do {                   \
+  } while (0)
+#endif
+
 // ------------------------------------------------------------------ element conversions
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(__bf16 x) { return (float)x; }

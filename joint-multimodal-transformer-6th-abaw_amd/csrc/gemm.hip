@@ -195,6 +195,7 @@ __device__ __forceinline__ void glds_tile(char* img, const T* base, int64_t ld, 
     const T* src;
     if constexpr (KMAJ) {
       const int gr = min(r0 + row, rows_lim - 1);
+      JMT_DCHECK(gr >= 0 && kloc + kk >= 0);
       src = base + (int64_t)gr * ld + kloc + kk;
     } else {
       int gm = r0 + row;
@@ -640,6 +641,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const GemmWor
           typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
           const u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
           // streaming (nontemporal) stores: measured 5-12% faster on the JMT shapes
+          JMT_DCHECK(m < p.M && n + 8 <= p.N);
           if (p.dbg & 4) *(u32x4*)(cp + rowo + n) = v;
           else __builtin_nontemporal_store(v, (u32x4*)(cp + rowo + n));
         }
@@ -684,6 +686,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const GemmWor
         const int n = n0 + wn * C::WTN + 16 * j + cq;
         if (n >= p.N) continue;
         const bool full4 = vec4 && n + 4 <= p.N;
+        JMT_DCHECK(m >= 0 && m < p.M && n >= 0);
         float x[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) x[e] = acc[i][j][e] * alpha + bias4[j][e] + bm;

@@ -177,6 +177,7 @@ __global__ __launch_bounds__(RB) void ln_fwd_vec_kernel(int64_t rows, const TI* 
                                                         float eps, TO* y, int64_t ldy,
                                                         float* mean, float* rstd) {
   constexpr int D = NV * 256;
+  JMT_DCHECK(ldx >= D && ldy >= D && (!rr || ldr >= D));
   const int lane = threadIdx.x & 63;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LNF_RPW;
   float gm[NV][4], bt[NV][4];

@@ -9,7 +9,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libjmt_hip.so")
+# JMT_LIB selects another build of the same ABI (csrc `make bounds`: build/bounds/libjmt_hip.so
+# with device-side index checks); default: the in-tree library
+LIB_PATH = os.environ.get("JMT_LIB") or os.path.join(_HERE, "libjmt_hip.so")
 
 F32, BF16, F16 = 0, 1, 2
 OK, ERR_ARG, ERR_HIP, ERR_UNSUPPORTED = 0, -1, -2, -3     # include/jmt.h
@@ -48,6 +50,7 @@ _PROTOS = {
     "jmt_abi_version": (c_int, []),
     "jmt_last_error": (C.c_char_p, []),
     "jmt_kernel_count": (c_int, []),
+    "jmt_bounds_violations": (C.c_longlong, [c_int]),
     "jmt_gemm": (c_int, [C.POINTER(GemmDesc), c_vp]),
     "jmt_gemm_workspace_bytes": (C.c_size_t, [c_int, c_int, c_int, c_int]),
     "jmt_gemm_plan_splits": (c_int, [c_int, c_int, c_int, c_int, c_int]),

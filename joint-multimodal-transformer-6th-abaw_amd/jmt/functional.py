@@ -1026,7 +1026,9 @@ class CELossFn(Function):
             lab = ops.cast(lab, torch.float32)
         w = None
         if weights is not None:
-            w = weights.to(device=dev, dtype=torch.float32).contiguous()
+            w = weights if (weights.device == dev and weights.dtype == torch.float32 and
+                            weights.is_contiguous()) else \
+                weights.to(device=dev, dtype=torch.float32).contiguous()
         stats = torch.empty(4, dtype=torch.float64, device=dev)
         ops.ce_stats(xc, lab, k, lo, hi, w, stats)
         world, stats_all = 1, stats

@@ -43,6 +43,8 @@ class CELoss(nn.Module):
         self.edges = np.linspace(*range, num=self.digitize_num + 1)
 
     def forward(self, x, y):
+        if self.weights is not None and self.weights.device != x.device:
+            self.weights = self.weights.to(x.device)      # once: later calls issue no copy
         return F.ce_loss(x, y.view(-1), self.digitize_num, rng=self.range, weights=self.weights,
                          group=jdist.loss_group())
 

@@ -66,7 +66,7 @@ def make_loss(mods, cls, *a, **k):
         torch.Tensor.cuda = orig
 
 
-def grad_record(out: dict, tag: str, named):
+def grad_record(out: dict, tag: str, named, rsample: bool = False):
     for name, t in named:
         g = t.grad
         key = f"{tag}/{name}"
@@ -77,6 +77,8 @@ def grad_record(out: dict, tag: str, named):
         out[key + ":norm"] = np.array(float(g.norm()))
         stride = max(1, g.numel() // N_SAMPLE)
         out[key + ":sample"] = g[::stride][:N_SAMPLE].float().numpy()
+        if rsample:
+            out[key + ":rsample"] = g[torch.from_numpy(spec.rsample_idx(name, g.numel()))].numpy()
 
 
 def checksum(x: np.ndarray) -> float:
@@ -172,9 +174,10 @@ def run_two_transformers(mods, out, c):
         h.remove()
     if taps:
         record_intermediates(out, tag, taps, B, T)
-    grad_record(out, tag, list(model.named_parameters()))
-    grad_record(out, tag, [("fc." + n, p) for n, p in fc.named_parameters()])
-    grad_record(out, tag, [("input.audio", a), ("input.video", v)])
+    rs = c.get("loss") == "proj"
+    grad_record(out, tag, list(model.named_parameters()), rs)
+    grad_record(out, tag, [("fc." + n, p) for n, p in fc.named_parameters()], rs)
+    grad_record(out, tag, [("input.audio", a), ("input.video", v)], rs)
 
     if c.get("train_steps"):
         # 3-step training trajectory (SURVEY.md §8c last paragraph): SGD nesterov, config lr etc.

@@ -95,3 +95,31 @@ def test_missing_library_raises(tmp_path, monkeypatch):
         _lib.load(str(tmp_path / "nope.so"))
     _lib._lib = None
     _lib.load()
+
+
+CSRC = os.path.join(REPO, "joint-multimodal-transformer-6th-abaw_amd", "csrc")
+
+
+def test_host_code_under_asan():
+    """SURVEY.md §5 sanitizer build: the library's host code (argument checks, planners, error
+    formatting, registration) compiled with AddressSanitizer (`make asan`: -Xarch_host
+    -fsanitize=address, device code at -O0 and never launched) and driven through every
+    validating entry point of include/jmt.h with invalid arguments (csrc/abi_check.cpp); ASan
+    must report nothing and every call must fail with an error message."""
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not installed")
+    jobs = str(min(8, os.cpu_count() or 4))
+    subprocess.run(["make", "-C", CSRC, "asan", "-j", jobs], check=True, timeout=1200,
+                   stdout=subprocess.DEVNULL)
+    exe = os.path.join(CSRC, "build", "asan", "abi_check")
+    syms = subprocess.run(["nm", exe], capture_output=True, text=True).stdout
+    assert "__asan_init" in syms or "__asan_report_load" in syms, "not ASan-instrumented"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0"))
+    assert "AddressSanitizer" not in r.stderr, r.stderr[-3000:]
+    assert r.returncode == 0 and "abi_check: ok" in r.stdout, (r.stdout, r.stderr[-2000:])
+
+
+def test_default_build_has_no_bounds_counters():
+    assert _lib.load().jmt_bounds_violations(0) == -1

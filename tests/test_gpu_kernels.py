@@ -1,6 +1,7 @@
 """Kernel-level numerics on the MI355X: every HIP kernel vs a plain PyTorch fp32 reference of the
 same op (computed from the same, already-rounded inputs), through the C-ABI."""
 import math
+import os
 
 import pytest
 import torch
@@ -683,3 +684,48 @@ def test_layernorm_bwd_dsum_matches_colsum(D):
                                                                               atol=1e-4)
     want = 1.0 + dx0.float().sum(0)
     assert (ds1 - want).abs().max().item() <= 1e-2 * want.abs().max().item() + 1e-3
+
+
+_BOUNDS_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                           "joint-multimodal-transformer-6th-abaw_amd", "jmt",
+                           "libjmt_hip_bounds.so")
+
+_BOUNDS_SCRIPT = r"""
+import sys, torch
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+from jmt import _lib, functional as JF
+from models.two_transformers import Two_transformers
+from models.fc_layer import FcLayer
+from losses.loss import CCCLoss
+lib = _lib.load()
+assert lib.jmt_bounds_violations(1) == 0
+for jm, fmt, B, T in (("TRANSFORMER", "FC", 4, 300), ("TRANSFORMER", "SELF_ATTEN", 2, 37),
+                      ("NONE", "FC", 8, 61)):
+    torch.manual_seed(0)
+    m = Two_transformers(0.0, 0.0, 1, 1, jm, fmt, 2048).cuda()
+    fc = FcLayer(1024, 512).cuda()
+    a = torch.randn(B, T, 1024, device="cuda"); v = torch.randn(B, T, 2048, device="cuda")
+    y = torch.rand(1, B * T, device="cuda") * 2 - 1
+    crit = CCCLoss(1)
+    for cd in (torch.bfloat16, torch.float32):
+        with JF.compute_mode(cd):
+            vo, ao = m(fc(a), v)
+            (crit(vo.reshape(1, -1), y) + crit(ao.reshape(1, -1), y)).backward()
+n = lib.jmt_bounds_violations(1)
+print("violations", n)
+sys.exit(0 if n == 0 else 3)
+"""
+
+
+@pytest.mark.skipif(not os.path.exists(_BOUNDS_LIB), reason="bounds build not present")
+def test_bounds_build_reports_no_violations():
+    """the device-side index-check build (csrc `make bounds`, JMT_DCHECK counters)
+    runs the TRANSFORMER/FC (T=300 tails), SELF_ATTEN and NONE models forward + backward in bf16
+    and fp32 with zero failed checks.  Runs in a child process with JMT_LIB pointing at it."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(repo, "joint-multimodal-transformer-6th-abaw_amd")
+    r = subprocess.run([sys.executable, "-c", _BOUNDS_SCRIPT, repo, pkg], capture_output=True,
+                       text=True, timeout=240, env=dict(os.environ, JMT_LIB=_BOUNDS_LIB))
+    assert r.returncode == 0 and "violations 0" in r.stdout, (r.stdout, r.stderr[-3000:])
