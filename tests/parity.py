@@ -134,7 +134,7 @@ def emulated(golden: dict, c: dict, cd) -> dict:
 # K_STRICT times as far from the fp32 reference as the rounding-emulating oracle on the SAME
 # quantity (no group / median floors), and never beyond an absolute ceiling: 5 % (bf16) / 2 %
 # (fp16) relative on predictions, losses and every parameter gradient; 9 % / 3.5 % on the
-# recorded intermediates and their gradients (8 sampled rows each) and the inputs' gradients.  Margins (bound / error) of every
+# recorded intermediates and their gradients (all rows) and the inputs' gradients.  Margins (bound / error) of every
 # quantity are reported by scripts/parity_report.py (profiles/r03_parity_error_model.txt).
 UNIT = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11}   # unit roundoff of 16-bit storage
 K_STRICT = 3.0
@@ -142,10 +142,41 @@ CEIL = {torch.bfloat16: {"param": 0.05, "out": 0.05, "inter": 0.09},
         torch.float16: {"param": 0.02, "out": 0.02, "inter": 0.035}}
 
 
+_REF_TAPS = {}
+
+
+def ref_taps(c: dict) -> dict:
+    """The fp32 oracle's intermediates of a case on ALL rows (cached).  The oracle reproduces the
+    reference goldens' 8 sampled rows to 1e-4 (tests/test_oracle.py); the strict suite compares
+    every row, because 16-bit errors of an intermediate gradient concentrate in the few rows
+    where a ReLU mask flips (chaotic: different rows for different roundings), so an 8-row
+    sample is hit-or-miss (scripts/r03/sa_probe2.py)."""
+    if c["tag"] not in _REF_TAPS:
+        from tests.oracle_cases import oracle_tt
+        torch.set_num_threads(min(16, max(1, len(os.sched_getaffinity(0)))))
+        _REF_TAPS[c["tag"]] = oracle_tt(c)["taps"]
+    return _REF_TAPS[c["tag"]]
+
+
+def _inter_all_rows(ref: dict, store: dict) -> dict:
+    errs = {}
+    for name, d in ref.items():
+        for kind in ("val", "grad"):
+            r = d[kind].double().cpu().reshape(-1, d[kind].shape[-1])
+            t = store.get(name, {}).get(kind)
+            if t is None:
+                errs[f"{name}:{kind}"] = float("inf")
+                continue
+            g = t.detach().double().cpu().reshape(r.shape)
+            errs[f"{name}:{kind}"] = float((g - r).norm() / max(float(r.norm()), 1e-30))
+    return errs
+
+
 def strict_errors(golden: dict, c: dict, vo, ao, l1, l2, grads, store) -> dict:
     """{quantity: relative error} of one run of a conditioned case: predictions (max-abs relative
-    to the largest |prediction|), the two losses (relative), every parameter / input gradient
-    (grad_errors), every recorded intermediate and its gradient (inter_errors)."""
+    to the largest |prediction|), the two losses, every parameter / input gradient
+    (grad_errors_rsample), every recorded intermediate and its gradient on all rows (vs the
+    fp32 oracle, ref_taps)."""
     tag = c["tag"]
     q = {}
     # the V and A predictions share one scale (valence / arousal in [-1, 1]): errors relative to
@@ -163,7 +194,7 @@ def strict_errors(golden: dict, c: dict, vo, ao, l1, l2, grads, store) -> dict:
         # the inputs' gradients are activation gradients (ceiling of the intermediates)
         q[("inter:" if k.startswith("input.") else "param:") + k] = e
     if c.get("inter"):
-        for k, e in inter_errors(golden, tag, store).items():
+        for k, e in _inter_all_rows(ref_taps(c), store).items():
             q["inter:" + k] = e
     return q
 
