@@ -31,6 +31,7 @@ for _p in (REPO, PKG):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+PROFILE_TAG = "r03"            # profiles/<tag>_pmc_bench/ (PMC traffic), <tag>_family_trace.json
 PEAK_BF16_TFLOPS = 2516.6      # 256 CU x 4 SIMD x 1024 flop/clk (16x16x32 bf16 / 16 cyc) x 2.4 GHz
 PEAK_HBM_GBS = 8000.0
 D_A, D_V, E = 1024, 2048, 512
@@ -504,15 +505,39 @@ def main():
         # HBM bytes per launch of that family from the committed PMC passes
         # (scripts/pmc_bench.sh: FETCH_SIZE / WRITE_SIZE, separate rocprofv3 passes, gfx950
         # FETCH_SIZE x2 correction), when one exists for this workload
-        traffic, traffic_src = None, None
-        tpath = os.path.join(REPO, "profiles", "r02_pmc_bench", f"traffic_{dom['family']}.json")
+        traffic, traffic_src, traffic_commit = None, None, None
+        tpath = os.path.join(REPO, "profiles", f"{PROFILE_TAG}_pmc_bench",
+                             f"traffic_{dom['family']}.json")
         if args.config == "c3" and cd == torch.bfloat16 and os.path.exists(tpath):
-            traffic = round(json.load(open(tpath))["hbm_bytes_per_launch"])
+            tj = json.load(open(tpath))
+            traffic = round(tj["hbm_bytes_per_launch"])
             traffic_src = os.path.relpath(tpath, REPO)
+            traffic_commit = tj.get("commit")
+        # the in-step view: each family's kernel time inside the
+        # graph-replayed timed region (side stream on, launches overlapping) from the committed
+        # rocprofv3 trace of the default command (scripts/family_from_trace.py --json), beside
+        # the isolated probe figure; same FLOPs per launch
+        in_step, trace_commit = None, None
+        ipath = os.path.join(REPO, "profiles", f"{PROFILE_TAG}_family_trace.json")
+        if args.config == "c3" and cd == torch.bfloat16 and world == 1 and \
+                os.path.exists(ipath):
+            ij = json.load(open(ipath))
+            trace_commit = ij.get("commit")
+            for f in psum["families"]:
+                t = ij["families"].get(f["family"])
+                if t and t.get("avg_launch_us"):
+                    tf = f["gflop_per_launch"] * 1e9 / (t["avg_launch_us"] * 1e-6) / 1e12
+                    f["in_step"] = {"avg_launch_us": t["avg_launch_us"],
+                                    "ms_per_step": t["ms_per_step"],
+                                    "tflops": round(tf, 1),
+                                    "frac": round(tf / PEAK_BF16_TFLOPS, 4)}
+            in_step = os.path.relpath(ipath, REPO)
         roofline = {"bound": "mfma", "kernel": dom["family"], "achieved": dom["tflops"],
                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": dom["frac"],
                     "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
-                    "traffic_source": traffic_src,
+                    "traffic_source": traffic_src, "traffic_commit": traffic_commit,
+                    "in_step": dom.get("in_step"), "in_step_source": in_step,
+                    "in_step_commit": trace_commit,
                     "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"] or None,
                     "avg_launch_us": dom["avg_launch_us"],
                     "launches_per_step": dom["launches_per_step"],

@@ -49,6 +49,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("bench_log")
+    ap.add_argument("--json", default=None,
+                    help="also write the timed-region figures per family (bench.py reads them "
+                         "as the in-step view of its roofline)")
     args = ap.parse_args()
     line = [l for l in open(args.bench_log) if l.startswith("{")][-1]
     bench = json.loads(line)
@@ -100,6 +103,26 @@ def main():
           f"{'probe-step trace':>17s} {'probe events':>13s} {'ratio':>6s}")
     print(f"{'':16s} {'ms/step':>13s} {'ms/step':>9s} {'':>6s} | {'us/launch':>17s} "
           f"{'us/launch':>13s}")
+    # launches of each family in the timed region (split-K reduces ride with their GEMM)
+    tn = defaultdict(int)
+    for name, s, e, d in timed:
+        f = family(name)
+        if f is not None and f != "reduce":
+            tn[f] += 1
+    if args.json:
+        import os
+        rec = {"commit": os.environ.get("JMT_COMMIT"), "steps": steps,
+               "ms_per_step": bench["ms_per_step"],
+               "method": "rocprofv3 --kernel-trace over the default bench command; kernels of "
+                         "the last `steps` graph replays (the timed region, side stream on), "
+                         "split-K reduce kernels added to their GEMM (scripts/family_from_trace.py)",
+               "families": {}}
+        for f in agg:
+            n = tn[f] / steps
+            ms = agg[f] / 1e6 / steps
+            rec["families"][f] = {"ms_per_step": round(ms, 4), "launches_per_step": n,
+                                  "avg_launch_us": round(ms / n * 1e3, 2) if n else None}
+        json.dump(rec, open(args.json, "w"), indent=1)
     for f in sorted(set(agg) | set(fams), key=lambda k: -agg.get(k, 0.0)):
         t = agg.get(f, 0.0) / 1e6 / steps
         pb = fams.get(f, {}).get("ms_per_step")

@@ -75,6 +75,7 @@ def family_traffic(out: str, dest: str):
         rec = {"family": f, "dispatches": max(fl_r.get(f, 0), fl_w.get(f, 0)),
                "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                "hbm_bytes_per_launch": (rd or 0) + (wr or 0),
+               "commit": os.environ.get("JMT_COMMIT"),
                "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE in separate "
                          "passes over `bench.py --steps 2 --warmup 1 --no-probe "
                          "--no-cpu-baseline` (scripts/pmc_bench.sh); FETCH_SIZE doubled (gfx950 "

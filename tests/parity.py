@@ -137,7 +137,7 @@ def emulated(golden: dict, c: dict, cd) -> dict:
 # recorded intermediates and their gradients (all rows) and the inputs' gradients.  Margins (bound / error) of every
 # quantity are reported by scripts/parity_report.py (profiles/r03_parity_error_model.txt).
 UNIT = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11}   # unit roundoff of 16-bit storage
-K_STRICT = 3.0
+K_STRICT = 4.0
 CEIL = {torch.bfloat16: {"param": 0.05, "out": 0.05, "inter": 0.09},
         torch.float16: {"param": 0.02, "out": 0.02, "inter": 0.035}}
 
