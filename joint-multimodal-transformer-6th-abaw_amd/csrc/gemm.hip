@@ -101,6 +101,12 @@ using Cfg11 = TileCfg<128, 128, 2, 2, 64, 3, 1, 1, 0, 3>;
 using Cfg20 = TileCfg<256, 256, 2, 4, 64, 4, 1, 1, 0, 0, 1>;
 // 128x128, 64-B K-tiles, 4 stages, interleaved issue, 2 blocks / CU
 using Cfg21 = TileCfg<128, 128, 2, 2, 64, 4, 1, 1, 0, 2, 1>;
+// 160x256 (8 waves of 80x64): the M = B*T = 19,200-row problems are 120 row tiles, so a
+// 512-wide output is 240 tiles — 0.94 of one wave on 256 CUs where the 256x256 tile leaves 150
+// (0.59 of a wave, 41 % of the CUs idle) and batched launches quantise to 94 % instead of 88 %.
+// K-major A only (the MN-major image swizzle needs a power-of-two row count); the 20 A
+// instructions of a K-tile are dealt round-robin over the 8 waves (glds_tile, dma_count).
+using Cfg30 = TileCfg<160, 256, 2, 4, 128, 2, 1, 1, 0>;
 // (256x256 over 4 waves — 2x2, 128x128 each, 256 accumulators per lane in AGPRs, 64-B K-tiles,
 // 4 stages, one block / CU: the macro tile hipBLASLt picks on these shapes, profiles/
 // r02_hipblaslt_reference.txt — compiled without spills but measured 1.45-1.65x slower than
@@ -183,13 +189,19 @@ __device__ __forceinline__ void glds_tile(char* img, const T* base, int64_t ld, 
                                           int r0, int kloc) {
   constexpr int V = Vec<T>::n;
   constexpr int NW = NT / 64;
-  constexpr int NI = ROWS * KB / 1024 / NW;
-  static_assert(NI >= 1, "tile too small for the block");
+  constexpr int TOT = ROWS * KB / 1024;    // wave-instructions (1 KiB each) of the image
+  constexpr bool EVEN = TOT % NW == 0;
+  constexpr int NI = (TOT + NW - 1) / NW;
+  static_assert(TOT >= NW || !EVEN, "tile too small for the block");
+  static_assert(ROWS * KB % 1024 == 0, "image not a whole number of wave-instructions");
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int q = w * NI + i;               // wave-instruction index = 1 KiB of the image
+    // even split: wave w owns instructions [w NI, (w+1) NI); otherwise they are dealt
+    // round-robin (wave w: w, w + NW, ...) and the last round is partial (tile_dma_count)
+    const int q = EVEN ? w * NI + i : i * NW + w;
+    if (!EVEN && q >= TOT) break;           // wave-uniform
     int row, kk;
     chunk_src<T, KMAJ, KB, ROWS>(q * 64 + lane, row, kk);
     const T* src;
@@ -249,11 +261,16 @@ template <typename T, bool KMAJ, int KB, int ROWS, int NT>
 __device__ __forceinline__ void stage_tile(char* img, const T* base, int64_t ld, int rows_lim,
                                            int r0, int k_lim, int kloc) {
   constexpr int V = Vec<T>::n;
-  constexpr int NC = ROWS * KB / 16 / NT;
+  constexpr int CH = ROWS * KB / 16;        // 16-B chunks of the image
+  constexpr int NC = (CH + NT - 1) / NT;
   uint4 r[NC];
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
     const int id = threadIdx.x + NT * i;
+    if (CH % NT != 0 && id >= CH) {
+      r[i] = make_uint4(0, 0, 0, 0);
+      continue;
+    }
     int row, kk;
     chunk_src<T, KMAJ, KB, ROWS>(id, row, kk);
     const int gr = r0 + row;
@@ -287,7 +304,8 @@ __device__ __forceinline__ void stage_tile(char* img, const T* base, int64_t ld,
     r[i] = v;
   }
 #pragma unroll
-  for (int i = 0; i < NC; ++i) *(uint4*)(img + (threadIdx.x + NT * i) * 16) = r[i];
+  for (int i = 0; i < NC; ++i)
+    if (CH % NT == 0 || threadIdx.x + NT * i < CH) *(uint4*)(img + (threadIdx.x + NT * i) * 16) = r[i];
 }
 
 // ------------------------------------------------------------------ fragment reads
@@ -437,15 +455,34 @@ __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB,
   }
 }
 
-__device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n) for small constants
+__device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n <= 16 (wave-uniform)
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
   }
+}
+
+// LDS-DMA instructions this wave issues per K-tile of one operand image of `tot` instructions
+// (glds_tile: an even split, or round-robin with a partial last round)
+template <int TOT, int NW>
+__device__ __forceinline__ int dma_count(int w) {
+  if constexpr (TOT % NW == 0) return TOT / NW;
+  else return w < TOT % NW ? TOT / NW + 1 : TOT / NW;
 }
 
 // wait until at most n (runtime, < 8) K-tiles of VMT DMA instructions each are outstanding
@@ -739,7 +776,10 @@ void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BKE = C::KB / (int)sizeof(T);         // K elements per tile
   constexpr int IA = C::BM * C::KB;                   // A image bytes
-  constexpr int VMT = (C::BM + C::BN) * C::KB / 1024 / (C::NT / 64);   // DMA instr / wave / tile
+  constexpr int NWV = C::NT / 64;
+  // LDS-DMA instructions per wave per K-tile (the same for every wave unless an image's count is
+  // not a multiple of the wave count, e.g. the 160-row tile: then it depends on the wave)
+  constexpr int VMT = ((C::BM + C::BN) * C::KB / 1024 + NWV - 1) / NWV;
 
   const int ntile = p.tiles_m * p.tiles_n;
   const GemmWork cur = decode_work<C>(
@@ -765,7 +805,9 @@ void gemm_kernel(GemmParams p) {
     for (int kt = 0; kt < nfull; ++kt) {
       if (kt + 1 < nfull) {
         issue_ktile<T, AK, BK, C>(p, smem, cur, kt + 1, (kt + 1) & 1);
-        wait_vm(VMT);                          // tile kt landed (one newer tile in flight)
+        // tile kt landed (one newer tile in flight)
+        const int wu = __builtin_amdgcn_readfirstlane(wid);
+        wait_vm(dma_count<C::BM * C::KB / 1024, NWV>(wu) + dma_count<C::BN * C::KB / 1024, NWV>(wu));
       } else {
         wait_vm(0);
       }
@@ -779,6 +821,8 @@ void gemm_kernel(GemmParams p) {
     // S-1 tiles in flight, one barrier per tile; tile kt+S-1's DMA is issued in pieces between
     // the MFMA rows of tile kt (buffer (kt-1) % S: freed by this iteration's barrier)
     static_assert(C::S >= 3 && C::S <= 5, "interleaved staging needs 3-5 stages");
+    static_assert(C::BM * C::KB / 1024 % NWV == 0 && C::BN * C::KB / 1024 % NWV == 0,
+                  "an uneven LDS-DMA split needs the 2-stage pipeline");
     constexpr int NIA = C::BM * C::KB / 1024 / (C::NT / 64);
     constexpr int NIB = C::BN * C::KB / 1024 / (C::NT / 64);
     constexpr int NR = C::KB / 64 * C::TM;            // MFMA rows per K-tile
@@ -833,6 +877,8 @@ void gemm_kernel(GemmParams p) {
     // S-1 tiles in flight, one barrier per tile: the barrier of iteration kt also certifies that
     // every wave finished computing tile kt-1, whose buffer receives tile kt+S-1.
     static_assert(C::S <= 9 && (C::S - 2) * VMT < 64, "wait_tiles covers up to 7 newer tiles");
+    static_assert(C::BM * C::KB / 1024 % NWV == 0 && C::BN * C::KB / 1024 % NWV == 0,
+                  "an uneven LDS-DMA split needs the 2-stage pipeline");
 #pragma unroll
     for (int i = 0; i < C::S - 1; ++i)
       if (i < nfull) issue_ktile<T, AK, BK, C>(p, smem, cur, i, i);
@@ -966,6 +1012,8 @@ template <typename T, typename O, bool AK, bool BK>
 static void launch_layout(const GemmParams& p, int cfg, dim3 grid, hipStream_t st) {
   switch (cfg) {
     case 5: launch_cfg<T, O, AK, BK, Cfg5>(p, grid, st); break;
+    case 30: if constexpr (AK) { launch_cfg<T, O, AK, BK, Cfg30>(p, grid, st); break; }
+             [[fallthrough]];
     case 10: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg10>(p, grid, st); break; }
              [[fallthrough]];
     case 11: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg11>(p, grid, st); break; }
@@ -995,6 +1043,7 @@ static void launch_t(const GemmParams& p, int ak, int bk, int cfg, dim3 grid, hi
 static void cfg_tile(int cfg, int& bm, int& bn) {
   switch (cfg) {
     case 5: case 20: bm = 256; bn = 256; break;
+    case 30: bm = 160; bn = 256; break;
     default: bm = 128; bn = 128; break;
   }
 }
@@ -1036,6 +1085,15 @@ static bool tile_ok(const TileModel& t, int M, int N) {
 // the grouped NN dgrads run fastest on the interleaved-DMA 256x256 tile (Cfg20: -2..-18 %), the
 // grouped NT forwards on the plain 256x256 tile (-2..-7 % vs the round-1 128x128 overrides).
 static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, int splits) {
+  // round 3: the 160x256 tile on the single (un-batched) B*T-row GEMMs — the 19,200-row output
+  // of N <= 1024 is 240 / 480 tiles instead of 150 / 300 of 256x256 (0.94 / 1.88 waves on 256
+  // CUs instead of 0.59 / 1.17): video linear fwd 69 -> 54 us, FcLayer fwd 42 -> 33, head dgrad
+  // 45 -> 36, K-concat stream dgrad 94 -> 84 (was Cfg11); and the grouped qkv forward (b3,
+  // N = 1536) 167 -> 161.  Batched N = 512 / 1024 launches stay on 256x256 (cfg 30 lost 6-15 %
+  // there: 1.76 / 3.5 waves already quantise well).  profiles/r03_gemm_tile160.jsonl
+  if (splits <= 1 && ak && M >= 4096 && K >= 512 && K % 64 == 0 &&
+      ((batch == 1 && N <= 1024) || (bk && batch == 3 && N == 1536 && K == 512)))
+    return 30;
   if (!ak && !bk && M >= 1536 && N >= 512 && batch >= 3 && K >= 8192)
     return 10;                                                   // split-K qkv wgrad
   if (!ak && !bk && batch == 6 && M == 1024 && N == 512 && K >= 8192)
@@ -1191,6 +1249,7 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   }
   int cfg = g_gemm_cfg;
   if (dt == JMT_F32 && cfg >= 10) cfg = 1;   // occupancy configs: 16-bit only
+  if (cfg == 30 && !d->a_kmajor) cfg = 5;    // 160-row tile: K-major A only
   if (!cfg) {
     int s_unused;
     plan(dt, d->M, d->N, d->K, batch0 * batch1, splits, cfg, s_unused);

@@ -43,6 +43,10 @@ def make_shapes(R):
         ("ca wgrad b6 TN 1024x512xR", 1024, 512, R, False, False, 6, F32, {"beta": 1.0}),
         ("ca wgrad b6 TN 512x512xR", 512, 512, R, False, False, 6, F32, {"beta": 1.0}),
         ("enc wgrad b3 TN 512x1536xR", 512, 1536, R, False, False, 3, F32, {"beta": 1.0}),
+        ("video linear fwd NT 512x2048", R, 512, 2048, True, True, 1, BF16, {}),
+        ("fc fwd NT 512x1024", R, 512, 1024, True, True, 1, BF16, {}),
+        ("pv dgrad NN 1024x512 b1", R, 1024, 512, True, False, 1, BF16, {}),
+        ("head dgrad NN 512x1024 b1", R, 512, 1024, True, False, 1, BF16, {}),
     ]
 
 

@@ -11,12 +11,13 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 tail -1 $OUT/smoke.log
 timeout -k 10 400 python bench.py > $OUT/bench_plain.log 2>&1 || { echo bench failed; tail $OUT/bench_plain.log; exit 1; }
 grep '^{' $OUT/bench_plain.log | tail -1 | cut -c1-300
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline > $OUT/bench_prof.log 2>&1 || { echo prof failed; tail $OUT/bench_prof.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format rocpd csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline > $OUT/bench_prof.log 2>&1 || { echo prof failed; tail $OUT/bench_prof.log; exit 1; }
 db=$(find $OUT/prof -name "*results.db" | head -1)
 python scripts/family_from_trace.py "$db" $OUT/bench_prof.log --json $OUT/family_trace.json > $OUT/family_check.txt 2>&1
 cat $OUT/family_check.txt
 find $OUT/prof -name "*.db" -delete
 find $OUT/prof -name "*kernel_trace.csv" -delete
+mkdir -p $OUT/pmc
 i=0
 for SET in "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
