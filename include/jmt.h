@@ -211,6 +211,26 @@ int jmt_copy2d(int src_dt, int dst_dt, int64_t rows, int64_t cols, const void* s
                int64_t src_rs, int64_t src_cs, void* dst, int64_t dst_rs, int64_t dst_cs,
                int accumulate, void* stream);
 
+/* ------------------------------------------------------------------ regressor output layers
+ * The second Linear(128, k) of the V and A regressors (two_transformers.py:104-114; k = 1, or
+ * the digitize_num bins of configs[4]'s head, k <= 24) for both heads at once: they read the
+ * halves of one hidden buffer h = [h_0 | h_1] (rows x 256, row stride ldh, bf16 / f16, ReLU
+ * applied); W2_g (k x 128) in h's dtype, b2_g fp32 (NULL = no bias).
+ * jmt_head_fwd: y_g[r][o] = sum_j h_g[r][j] W2_g[o][j] + b2_g[o] (fp32 accumulation), y_g at row
+ *   stride ldy in y_dt (f32 or h's dtype).
+ * jmt_head_bwd: dh[r][128 g + j] = [h > 0] sum_o gy_g[r][o] W2_g[o][j] (h's dtype, row stride
+ *   lddh); dw2_g += sum_r gy_g[r][o] h_g[r][j] and db2_g += sum_r gy_g[r][o] (fp32, NULL =
+ *   skip), deterministic two-phase sums through `partials`
+ *   (jmt_head_bwd_workspace_bytes(rows) bytes). */
+int jmt_head_fwd(int h_dt, int y_dt, int64_t rows, int hid, int k, const void* h, int64_t ldh,
+                 const void* w2_0, const void* w2_1, const float* b2_0, const float* b2_1,
+                 void* y_0, void* y_1, int64_t ldy, void* stream);
+int jmt_head_bwd(int h_dt, int gy_dt, int64_t rows, int hid, int k, const void* h, int64_t ldh,
+                 const void* w2_0, const void* w2_1, const void* gy_0, const void* gy_1,
+                 int64_t ldgy, void* dh, int64_t lddh, float* dw2_0, float* dw2_1, float* db2_0,
+                 float* db2_1, float* partials, void* stream);
+size_t jmt_head_bwd_workspace_bytes(int64_t rows);
+
 /* ------------------------------------------------------------------ CCC losses
  * kind 0: losses/loss.py:8-32 CCCLoss (digitize_num k; k>1: pred is (n,k) logits, softmax over
  *         bins = linspace(range) first)

@@ -100,6 +100,11 @@ _PROTOS = {
     "jmt_mask_indices": (c_int, [c_i64, c_vp, c_f, c_vp, c_vp, c_vp]),
     "jmt_vp_scatter": (c_int, [c_i64] + [c_vp] * 9 + [c_f, c_i64] + [c_vp] * 6),
     "jmt_vp_smooth": (c_int, [c_i64, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "jmt_head_fwd": (c_int, [c_int, c_int, c_i64, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_vp,
+                             c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "jmt_head_bwd": (c_int, [c_int, c_int, c_i64, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_vp,
+                             c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "jmt_head_bwd_workspace_bytes": (C.c_size_t, [c_i64]),
     "jmt_ce_stats": (c_int, [c_int, c_i64, c_int, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp]),
     "jmt_ce_finish": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp]),
     "jmt_ce_bwd": (c_int, [c_int, c_i64, c_int, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_vp,

@@ -408,6 +408,7 @@ def mlp(x, W1, b1, W2, b2, out_dtype=None):
 
 
 _pair_mlp = {"on": os.environ.get("JMT_PAIR_MLP", "1") != "0"}
+_fused_head_on = {"on": os.environ.get("JMT_FUSED_HEAD", "1") != "0"}
 
 
 def pair_mlps_enabled() -> bool:
@@ -443,17 +444,29 @@ class MLPPairFn(Function):
                  c=[h.data_ptr()], ldc=ldh, batch0=2, sA=(0, 0), sC=(hid, 0),
                  bias_tab=[b1a, b1b], bias_mode=1, relu=True, device=h.device)
         odt = out_dtype if out_dtype is not None else cd
-        # both second layers: one launch over the halves of h (2-entry weight / bias / out table)
         ys = [L.like(nout, odt), L.like(nout, odt)]
         W2c = [weight_as(W2a, cd), weight_as(W2b, cd)]
-        ops.gemm(M=L.rows, N=nout, K=hid, ab_dtype=_dc(cd), c_dtype=_dc(odt),
-                 a=[h.data_ptr()], lda=ldh, a_kmajor=True, sA=(hid, 0),
-                 b=[w.data_ptr() for w in W2c], ldb=hid, b_kmajor=True, b_mode=1,
-                 c=[y.data_ptr() for y in ys], ldc=_ld(ys[0], L.perm), c_mode=1, batch0=2,
-                 bias_tab=[b2a, b2b], bias_mode=1, device=h.device)
+        if MLPPairFn._fused_head(cd, hid, nout):
+            # both second layers as one row kernel over [h_a | h_b] (csrc/head.hip)
+            ops.head_fwd(h, ldh, L.rows, nout, W2c, (b2a, b2b), ys, _ld(ys[0], L.perm))
+        else:
+            # both second layers: one GEMM launch over the halves of h (2-entry tables)
+            ops.gemm(M=L.rows, N=nout, K=hid, ab_dtype=_dc(cd), c_dtype=_dc(odt),
+                     a=[h.data_ptr()], lda=ldh, a_kmajor=True, sA=(hid, 0),
+                     b=[w.data_ptr() for w in W2c], ldb=hid, b_kmajor=True, b_mode=1,
+                     c=[y.data_ptr() for y in ys], ldc=_ld(ys[0], L.perm), c_mode=1, batch0=2,
+                     bias_tab=[b2a, b2b], bias_mode=1, device=h.device)
         ctx.save_for_backward(W1a, b1a, W2a, b2a, W1b, b1b, W2b, b2b, L.t, h)
         ctx.meta = (cd, L, x.dtype, odt)
         return ys[0], ys[1]
+
+    @staticmethod
+    def _fused_head(cd, hid, nout) -> bool:
+        """The output layers run as csrc/head.hip row kernels (16-bit compute, hidden width 128,
+        k <= 24: the V / A regressors and configs[4]'s 20-bin head); JMT_FUSED_HEAD=0 keeps
+        the GEMM form."""
+        return (_fused_head_on["on"] and cd != torch.float32 and hid == ops.HEAD_HID and
+                nout <= ops.HEAD_KMAX)
 
     @staticmethod
     def _w2_grads(Gs, hh, ldhh, hid, nout, W2s, b2s, dt, dev):
@@ -492,6 +505,35 @@ class MLPPairFn(Function):
             if gy is None:
                 gy = torch.zeros(L.like(nout, odt).shape, dtype=odt, device=dev)
             gys.append(gy)
+        if MLPPairFn._fused_head(cd, hid, nout):
+            # dh (ReLU-masked) and both output layers' weight / bias gradients in one row
+            # kernel from the fp32 loss gradient (csrc/head.hip), then the input gradient as ONE
+            # K-concatenated GEMM dx = [dh_a | dh_b] [W1a; W1b] (one rounding of the sum of both
+            # heads' contributions, no separate add)
+            gdt = torch.float32 if odt == torch.float32 else cd
+            G2 = [_match(gy, Rows(L.like(nout, gdt)), gdt) for gy in gys]
+            if G2[1].ld != G2[0].ld or G2[1].perm != G2[0].perm:
+                G2[1] = _match(G2[1].t, G2[0], gdt)
+            W2c = [weight_as(W2a, cd), weight_as(W2b, cd)]
+            dw2 = [_grad_buffer(W2a), _grad_buffer(W2b)]
+            db2 = [_grad_buffer(b2a), _grad_buffer(b2b)]
+            ops.head_bwd(h, ldh, L.rows, nout, W2c, [G.t for G in G2], G2[0].ld, dh, ldh, dw2,
+                         db2)
+            _grad_done(W2a, W2b, b2a, b2b)
+            dx = None
+            if ctx.needs_input_grad[9]:
+                dx = L.like(L.F, cd)
+                W1c = [weight_as(W1a, cd), weight_as(W1b, cd)]
+                ops.gemm(M=L.rows, N=L.F, K=2 * hid, ab_dtype=_dc(cd), c_dtype=_dc(cd),
+                         a=[dh.data_ptr()], lda=ldh, a_kmajor=True,
+                         b=[w.data_ptr() for w in W1c], ldb=L.F, b_kmajor=False, b_mode=2,
+                         b_kseg=hid, c=[dx.data_ptr()], ldc=_ld(dx, L.perm), device=dev)
+                if xdt != cd:
+                    dx = _cast_keep_layout(dx, xdt)
+            streams.run_side(lambda: MLPPairFn._w1_grads(dh, ldh, xin, L, hid, cd, dev,
+                                                         (W1a, W1b), (b1a, b1b)),
+                             reads=(dh, xin))
+            return (None,) * 9 + (dx,)
         Gys = [_match(gy, Rows(L.like(nout, cd)), cd) for gy in gys]
         if nout == 1 or Gys[0].ld == Gys[1].ld:
             # both second-layer input gradients (ReLU-masked) in one launch into [dh_a | dh_b]
@@ -531,28 +573,32 @@ class MLPPairFn(Function):
             if xdt != cd:
                 dx = _cast_keep_layout(dx, xdt)
 
-        def w1_grads():         # one grouped wgrad launch + one grouped column-sum launch pair
-            gws = []
-            for W in (W1a, W1b):
-                g = _grad_buffer(W)
-                gws.append(g if g is not None else torch.zeros_like(W))
-            ops.gemm(M=hid, N=L.F, K=L.rows, ab_dtype=_dc(cd), c_dtype=F32,
-                     a=[dh.data_ptr()], lda=ldh, a_kmajor=False,
-                     b=[xin.data_ptr()], ldb=L.ld, b_kmajor=False,
-                     c=[g.data_ptr() for g in gws], ldc=L.F, c_mode=1, batch0=2,
-                     sA=(hid, 0), sB=(0, 0), beta=1.0, device=dev)
-            _grad_done(W1a, W1b)
-            dbs = []
-            for b in (b1a, b1b):
-                gb = _grad_buffer(b)
-                dbs.append(gb if gb is not None else torch.empty(hid, dtype=torch.float32,
-                                                                 device=dev))
-            ops.colsum_grouped(dh.data_ptr(), _dc(cd), 2, ldh, hid, L.rows, hid, dbs,
-                               beta_acc=True, device=dev)
-            _grad_done(b1a, b1b)
-
-        streams.run_side(w1_grads, reads=(dh, xin))
+        streams.run_side(lambda: MLPPairFn._w1_grads(dh, ldh, xin, L, hid, cd, dev, (W1a, W1b),
+                                                     (b1a, b1b)),
+                         reads=(dh, xin))
         return (None,) * 9 + (dx,)
+
+    @staticmethod
+    def _w1_grads(dh, ldh, xin, L, hid, cd, dev, W1s, b1s):
+        """One grouped wgrad launch + one grouped column-sum launch pair (side stream)."""
+        gws = []
+        for W in W1s:
+            g = _grad_buffer(W)
+            gws.append(g if g is not None else torch.zeros_like(W))
+        ops.gemm(M=hid, N=L.F, K=L.rows, ab_dtype=_dc(cd), c_dtype=F32,
+                 a=[dh.data_ptr()], lda=ldh, a_kmajor=False,
+                 b=[xin.data_ptr()], ldb=L.ld, b_kmajor=False,
+                 c=[g.data_ptr() for g in gws], ldc=L.F, c_mode=1, batch0=2,
+                 sA=(hid, 0), sB=(0, 0), beta=1.0, device=dev)
+        _grad_done(*W1s)
+        dbs = []
+        for b in b1s:
+            gb = _grad_buffer(b)
+            dbs.append(gb if gb is not None else torch.empty(hid, dtype=torch.float32,
+                                                             device=dev))
+        ops.colsum_grouped(dh.data_ptr(), _dc(cd), 2, ldh, hid, L.rows, hid, dbs,
+                           beta_acc=True, device=dev)
+        _grad_done(*b1s)
 
 
 def mlp_pair(x, mlp_a, mlp_b, out_dtype=None):

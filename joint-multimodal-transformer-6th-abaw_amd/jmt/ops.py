@@ -304,6 +304,28 @@ def ccc_finish(kind, world, stats_all, bs, eps, loss, coef):
               coef.data_ptr(), stream())
 
 
+HEAD_HID, HEAD_KMAX = 128, 24      # csrc/head.hip
+
+
+def head_fwd(h, ldh, rows, k, w2, b2, ys, ldy):
+    """Both regressors' output layers (csrc/head.hip jmt_head_fwd)."""
+    p = lambda t: t.data_ptr() if t is not None else None
+    _lib.call("jmt_head_fwd", dt(h), dt(ys[0]), rows, HEAD_HID, k, h.data_ptr(), ldh,
+              w2[0].data_ptr(), w2[1].data_ptr(), p(b2[0]), p(b2[1]), ys[0].data_ptr(),
+              ys[1].data_ptr(), ldy, stream())
+
+
+def head_bwd(h, ldh, rows, k, w2, gys, ldgy, dh, lddh, dw2, db2):
+    """dh (ReLU-masked) and += weight / bias gradients of both output layers (jmt_head_bwd)."""
+    p = lambda t: t.data_ptr() if t is not None else None
+    nbytes = _lib.load().jmt_head_bwd_workspace_bytes(rows)
+    ws = torch.empty(max(1, nbytes // 4), dtype=torch.float32, device=h.device)
+    _lib.call("jmt_head_bwd", dt(h), dt(gys[0]), rows, HEAD_HID, k, h.data_ptr(), ldh,
+              w2[0].data_ptr(), w2[1].data_ptr(), gys[0].data_ptr(), gys[1].data_ptr(), ldgy,
+              dh.data_ptr(), lddh, p(dw2[0]), p(dw2[1]), p(db2[0]), p(db2[1]), ws.data_ptr(),
+              stream())
+
+
 def ce_stats(x, label, k, lo, hi, weights, stats):
     n = x.numel() // k
     _lib.call("jmt_ce_stats", dt(x), n, k, x.data_ptr(), label.data_ptr(), lo, hi,

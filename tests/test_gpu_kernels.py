@@ -729,3 +729,43 @@ def test_bounds_build_reports_no_violations():
     r = subprocess.run([sys.executable, "-c", _BOUNDS_SCRIPT, repo, pkg], capture_output=True,
                        text=True, timeout=240, env=dict(os.environ, JMT_LIB=_BOUNDS_LIB))
     assert r.returncode == 0 and "violations 0" in r.stdout, (r.stdout, r.stderr[-3000:])
+
+
+@pytest.mark.parametrize("k", [1, 20])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_head_kernels_vs_torch(k, dt):
+    """csrc/head.hip: both regressors' output layers (Linear(128, k) on the halves of one
+    ReLU'd hidden buffer, two_transformers.py:104-114) forward, ReLU-masked input gradient and
+    fp32 weight / bias gradients (+= into the buffers) vs torch fp32 on the same 16-bit h and
+    W2; ragged row count, padded row strides."""
+    from jmt import ops
+    g = torch.Generator(device=DEV).manual_seed(11)
+    rows, ldh = 1237, 264
+    h = torch.relu(torch.randn(rows, ldh, device=DEV, generator=g)).to(dt)
+    W2 = [(torch.randn(k, 128, device=DEV, generator=g) * 0.1).to(dt) for _ in range(2)]
+    b2 = [torch.randn(k, device=DEV, generator=g) for _ in range(2)]
+    ldy = k + 3
+    ys = [torch.full((rows, ldy), float("nan"), device=DEV) for _ in range(2)]
+    ops.head_fwd(h, ldh, rows, k, W2, b2, ys, ldy)
+    for i in range(2):
+        ref = h[:, 128 * i:128 * (i + 1)].float() @ W2[i].float().t() + b2[i]
+        err = (ys[i][:, :k] - ref).abs().max().item()
+        assert err <= 1e-5 * max(1.0, ref.abs().max().item()), (i, err)
+        assert torch.isnan(ys[i][:, k:]).all()
+    gy = [torch.randn(rows, ldy, device=DEV, generator=g) for _ in range(2)]
+    dh = torch.full((rows, ldh), float("nan"), device=DEV).to(dt)
+    dw = [torch.ones(k, 128, device=DEV) for _ in range(2)]      # accumulated into
+    db = [torch.ones(k, device=DEV) for _ in range(2)]
+    ops.head_bwd(h, ldh, rows, k, W2, gy, ldy, dh, ldh, dw, db)
+    tol = 2 ** -7 if dt == torch.bfloat16 else 2 ** -10
+    for i in range(2):
+        hh = h[:, 128 * i:128 * (i + 1)].float()
+        G = gy[i][:, :k]
+        ref_dh = (G @ W2[i].float()) * (hh > 0)
+        err = (dh[:, 128 * i:128 * (i + 1)].float() - ref_dh).abs().max().item()
+        assert err <= tol * max(1.0, ref_dh.abs().max().item()), (i, err)
+        rw = 1.0 + G.t() @ hh
+        assert (dw[i] - rw).abs().max().item() <= 1e-4 * rw.abs().max().item()
+        rb = 1.0 + G.sum(0)
+        assert (db[i] - rb).abs().max().item() <= 1e-4 * max(1.0, rb.abs().max().item())
+    assert torch.isnan(dh[:, 256:].float()).all(), "wrote past the two heads"
