@@ -2,8 +2,9 @@
 the two separate MLPFn calls it replaces, on a seq-first (T, B, E) input as the model feeds it:
 fp32 bit-exact forward and input gradient (same per-element arithmetic, the two input gradients
 summed by the same add autograd uses), weight / bias gradients within fp32 summation-order noise
-(the grouped weight-gradient launch may pick another split-K); 16-bit within a few units in the
-last place of the separate path."""
+(the grouped weight-gradient launch may pick another split-K); 16-bit: both paths against the fp32
+result, the pair (csrc/head.hip output layers, one K-concatenated input-gradient GEMM) at least as
+accurate as the separate path."""
 import pytest
 import torch
 
@@ -48,17 +49,27 @@ def test_mlp_pair_matches_two_mlps(cd, k):
         got = _run(True, cd, x0, va, aa, k)
     finally:
         JF.set_pair_mlps(True)
-    for r, g in zip(ref[:3], got[:3]):
+    if cd == torch.float32:
+        for r, g in zip(ref[:3], got[:3]):
+            assert r.shape == g.shape and torch.equal(r, g)
+        for r, g in zip(ref[3], got[3]):
+            scale = max(1.0, float(r.abs().max()))
+            assert float((r - g).abs().max()) <= 1e-5 * scale, float((r - g).abs().max())
+        return
+    # 16-bit: the pair's output layers run as csrc/head.hip row kernels from the fp32 loss
+    # gradient and its input gradient is one K-concatenated GEMM (fewer roundings than the two
+    # MLPFn calls): both paths against the fp32 result, the pair at least as accurate (x1.5)
+    try:
+        ref32 = _run(False, torch.float32, x0, va, aa, k)
+    finally:
+        JF.set_pair_mlps(True)
+    u = 2 ** -8 if cd == torch.bfloat16 else 2 ** -11
+    for r32, r, g in zip(list(ref32[:3]) + ref32[3], list(ref[:3]) + ref[3],
+                         list(got[:3]) + got[3]):
         assert r.shape == g.shape
-        if cd == torch.float32:
-            assert torch.equal(r, g)
-        else:
-            tol = 4 * (2 ** -8 if cd == torch.bfloat16 else 2 ** -11) * float(r.abs().max())
-            assert float((r - g).abs().max()) <= tol
-    for r, g in zip(ref[3], got[3]):
-        scale = max(1.0, float(r.abs().max()))
-        tol = 1e-5 if cd == torch.float32 else 2e-3
-        assert float((r - g).abs().max()) <= tol * scale, float((r - g).abs().max())
+        e_sep = float((r.float() - r32).norm()) / float(r32.norm())
+        e_pair = float((g.float() - r32).norm()) / float(r32.norm())
+        assert e_pair <= 1.5 * max(e_sep, u), (e_pair, e_sep)
 
 
 def test_two_transformers_uses_the_pair():
