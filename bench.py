@@ -189,7 +189,7 @@ class FamilyProbe:
                         "gflop_per_launch": round(d["flops"] / d["launches"] / 1e9, 3),
                         "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
                         "tflops": round(tf, 1), "frac": round(tf / PEAK_BF16_TFLOPS, 4)})
-            if f.startswith("small_attn"):          # HBM-bound family: bytes, not flops
+            if f.startswith(("small_attn", "attn_short")):   # HBM-bound families: bytes
                 gbs = d["bytes"] / (d["ms"] * 1e-3) / 1e9
                 out[-1].update({"bound": "hbm", "gbps": round(gbs, 1),
                                 "hbm_frac": round(gbs / PEAK_HBM_GBS, 4)})

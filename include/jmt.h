@@ -169,6 +169,28 @@ int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* go, i
                  void* ds_out, int64_t ldp, void* dq, int64_t sdq_l, int64_t sdq_n, float scale,
                  void* stream);
 
+/* Fused attention over short sequences, the whole backward in one kernel (Lq, Lk <= 32, 16-bit,
+ * dh = 512; the batch-axis self-attention of mm_transformers.py:119-146 at B = 32 and every
+ * attention of the T = 16 real-data configuration): same element addressing as jmt_attn_*,
+ * one block per (n, h).  jmt_attn_short_supported(dt, dh, Lq, Lk) != 0 for the covered shapes.
+ * jmt_attn_short_fwd: as jmt_attn_fwd (o and lse; bitwise the same values).
+ * jmt_attn_short_bwd: dq = dS K, dk = dS^T Q, dv = P^T dO with P recomputed from lse and
+ *   dS = scale * P o (dO V^T - rowsum(dO o O)); dq/dk/dv overwritten (they may be column slices
+ *   of one buffer); no P / dS leave the chip (replaces jmt_attn_bwd + the two jmt_gemm calls).
+ *   Rows 16-B aligned, strides multiples of 8.  (ABI 3, round 3 addition.) */
+int jmt_attn_short_supported(int dt, int dh, int Lq, int Lk);
+int jmt_attn_short_fwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* q, int64_t sq_l,
+                       int64_t sq_n, const void* k, int64_t sk_l, int64_t sk_n, const void* v,
+                       int64_t sv_l, int64_t sv_n, void* o, int64_t so_l, int64_t so_n,
+                       float scale, float* lse, void* stream);
+int jmt_attn_short_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* go,
+                       int64_t sgo_l, int64_t sgo_n, const void* o, int64_t so_l, int64_t so_n,
+                       const void* q, int64_t sq_l, int64_t sq_n, const void* k, int64_t sk_l,
+                       int64_t sk_n, const void* v, int64_t sv_l, int64_t sv_n, const float* lse,
+                       void* dq, int64_t sdq_l, int64_t sdq_n, void* dk, int64_t sdk_l,
+                       int64_t sdk_n, void* dv, int64_t sdv_l, int64_t sdv_n, float scale,
+                       void* stream);
+
 /* Attention over short sequences (Lq, Lk <= 8; E = H*dh = 512, E/8/H a power of two, dt any of
  * fp32/bf16/fp16): the SELF_ATTEN head's 6-token sequences (mm_multi_transformers.py:169-199)
  * and intra-modal fusion's 2-token ones (intra_modal_transformer_fusion.py:93-108), same element

@@ -79,6 +79,14 @@ _PROTOS = {
     "jmt_attn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp,
                              c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                              c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_f, c_vp]),
+    "jmt_attn_short_supported": (c_int, [c_int, c_int, c_int, c_int]),
+    "jmt_attn_short_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
+                                   c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
+                                   c_f, c_vp, c_vp]),
+    "jmt_attn_short_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
+                                   c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
+                                   c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                   c_i64, c_vp, c_i64, c_i64, c_f, c_vp]),
     "jmt_noop": (c_int, [c_vp]),
     "jmt_small_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
                                    c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,

@@ -787,9 +787,15 @@ def attn_forward(q_src, k_src, v_src, E, H, qcol, kcol, vcol):
     bS = (H * Lq * ldS, Lq * ldS)
     scale = 1.0 / math.sqrt(dh)
     o = Rows(q_src).like(E, cd)
-    small = ops.small_attn_ok(E, H, Lq, Lk) and all(
-        _small_aligned(t, c, cd) for t, c in ((q_src, qcol), (k_src, kcol), (v_src, vcol), (o, 0)))
-    fused = "small" if small else (cd != torch.float32 and ops.attn_supported(_dc(cd), dh))
+    aligned = all(_small_aligned(t, c, cd)
+                  for t, c in ((q_src, qcol), (k_src, kcol), (v_src, vcol), (o, 0)))
+    small = ops.small_attn_ok(E, H, Lq, Lk) and aligned
+    # Lq, Lk <= 32 (the batch-axis attention of wo_JR, the T = 16 real-data windows): one block
+    # per sequence, and the backward computes dK / dV in the same kernel (attn_short.hip)
+    short = (not small and cd != torch.float32 and aligned and
+             ops.attn_short_ok(_dc(cd), dh, Lq, Lk))
+    fused = "small" if small else ("short" if short else
+                                   (cd != torch.float32 and ops.attn_supported(_dc(cd), dh)))
     if small:
         # short sequences (SELF_ATTEN head, intra-modal fusion): one wave per sequence, the
         # fp32 probabilities (N*H*Lq*Lk floats) kept for the backward (small_attn.hip)
@@ -804,7 +810,8 @@ def attn_forward(q_src, k_src, v_src, E, H, qcol, kcol, vcol):
         # one kernel: scores stay on chip (attn.hip); only lse is kept for the backward, which
         # recomputes the probabilities
         lse = torch.empty(N * H * Lq, dtype=torch.float32, device=dev)
-        ops.attn_fwd(_dc(cd), N, H, Lq, Lk, dh,
+        (ops.attn_short_fwd if fused == "short" else ops.attn_fwd)(
+                     _dc(cd), N, H, Lq, Lk, dh,
                      _ptr(q_src, qcol), (q_src.stride(0), q_src.stride(1)),
                      _ptr(k_src, kcol), (k_src.stride(0), k_src.stride(1)),
                      _ptr(v_src, vcol), (v_src.stride(0), v_src.stride(1)),
@@ -841,7 +848,7 @@ def attn_backward(saved, go, dq, dk, dv):
     if fused and not _small_aligned(go, 0, cd):
         go = go.clone(memory_format=torch.contiguous_format)
         so_l, so_n = go.stride(0), go.stride(1)
-    if fused == "small":
+    if fused in ("small", "short"):
         # the kernel's layout contract covers the gradient buffers too: a misaligned one is
         # written through an aligned (contiguous) temporary and copied back.  Aliased buffers
         # (packed qkv) share one temporary.
@@ -854,11 +861,17 @@ def attn_backward(saved, go, dq, dk, dv):
             if key not in tmps:
                 tmps[key] = (buf, buf.clone(memory_format=torch.contiguous_format))
             outs.append((tmps[key][1], col))
-        ops.small_attn_bwd(_dc(cd), N, H, Lq, Lk, E, go.data_ptr(), (so_l, so_n),
-                           _ptr(q_src, qcol), (sq_l, sq_n), _ptr(k_src, kcol), (sk_l, sk_n),
-                           _ptr(v_src, vcol), (sv_l, sv_n), P,
-                           *[a for t, c in outs for a in (_ptr(t, c), (t.stride(0), t.stride(1)))],
-                           scale)
+        gouts = [a for t, c in outs for a in (_ptr(t, c), (t.stride(0), t.stride(1)))]
+        if fused == "small":
+            ops.small_attn_bwd(_dc(cd), N, H, Lq, Lk, E, go.data_ptr(), (so_l, so_n),
+                               _ptr(q_src, qcol), (sq_l, sq_n), _ptr(k_src, kcol), (sk_l, sk_n),
+                               _ptr(v_src, vcol), (sv_l, sv_n), P, *gouts, scale)
+        else:
+            # P recomputed from lse; dQ, dK and dV from one kernel (no P / dS in HBM)
+            ops.attn_short_bwd(_dc(cd), N, H, Lq, Lk, dh, go.data_ptr(), (so_l, so_n),
+                               o.data_ptr(), (o.stride(0), o.stride(1)),
+                               _ptr(q_src, qcol), (sq_l, sq_n), _ptr(k_src, kcol), (sk_l, sk_n),
+                               _ptr(v_src, vcol), (sv_l, sv_n), lse, *gouts, scale)
         for buf, tmp in tmps.values():
             buf.copy_(tmp)
         return

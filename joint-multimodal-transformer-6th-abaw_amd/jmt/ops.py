@@ -217,6 +217,41 @@ def attn_bwd(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k_ptr, 
             launch)
 
 
+def attn_short_ok(dtype: int, dh: int, Lq: int, Lk: int) -> bool:
+    """Shapes the one-block-per-sequence fused kernels cover (jmt_attn_short_*: 16-bit, dh = 512,
+    Lq, Lk <= 32); off with JMT_ATTN_FUSED=0 or JMT_ATTN_SHORT=0 (A/B switch)."""
+    return (_attn_fused["on"] and _attn_short["on"] and
+            bool(_lib.load().jmt_attn_short_supported(dtype, dh, Lq, Lk)))
+
+
+_attn_short = {"on": os.environ.get("JMT_ATTN_SHORT", "1") != "0"}
+
+
+def attn_short_fwd(dtype, N, H, Lq, Lk, dh, q_ptr, sq, k_ptr, sk, v_ptr, sv, o_ptr, so, scale,
+                   lse):
+    """jmt_attn_fwd's result (o, lse) for Lq, Lk <= 32: one block per (n, h)."""
+    launch = lambda: _lib.call("jmt_attn_short_fwd", dtype, N, H, Lq, Lk, dh, q_ptr, sq[0], sq[1],
+                               k_ptr, sk[0], sk[1], v_ptr, sv[0], sv[1], o_ptr, so[0], so[1],
+                               scale, lse.data_ptr(), stream())
+    es = 4 if dtype == F32 else 2
+    _hooked({"family": "attn_short_fwd", "flops": 4.0 * N * H * Lq * Lk * dh,
+             "bytes": float(N * H) * ((2 * Lq + 2 * Lk) * dh * es + 4 * Lq)}, launch)
+
+
+def attn_short_bwd(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k_ptr, sk, v_ptr,
+                   sv, lse, dq_ptr, sdq, dk_ptr, sdk, dv_ptr, sdv, scale):
+    """dQ, dK, dV of attn_short_fwd in one kernel (P recomputed from lse; no P / dS in HBM)."""
+    launch = lambda: _lib.call("jmt_attn_short_bwd", dtype, N, H, Lq, Lk, dh, go_ptr, sgo[0],
+                               sgo[1], o_ptr, so[0], so[1], q_ptr, sq[0], sq[1], k_ptr, sk[0],
+                               sk[1], v_ptr, sv[0], sv[1], lse.data_ptr(), dq_ptr, sdq[0], sdq[1],
+                               dk_ptr, sdk[0], sdk[1], dv_ptr, sdv[0], sdv[1], scale, stream())
+    # algorithmic: dP, dQ, dK, dV (the P recompute is not counted); bytes: q, o, dO, k, v, lse
+    # read, dq, dk, dv written
+    es = 4 if dtype == F32 else 2
+    _hooked({"family": "attn_short_bwd", "flops": 8.0 * N * H * Lq * Lk * dh,
+             "bytes": float(N * H) * ((4 * Lq + 4 * Lk) * dh * es + 4 * Lq)}, launch)
+
+
 SMALL_ATTN_MAX_L = 8
 
 

@@ -6,7 +6,10 @@
 * reference-relative suite (spec.TT_CASES, check_vs_ref16): GPU vs the reference's own autocast
   and the emulating oracle on prediction / loss / median and max parameter-gradient error.
 
-    python scripts/parity_report.py > gpurun_out/parity_report.jsonl"""
+    python scripts/parity_report.py [--dump DIR] > gpurun_out/parity_report.jsonl
+
+--dump DIR also writes every quantity's GPU and emulated error per (case, dtype) and, for the
+mutations of tests/test_gpu_models.py, the mutated GPU errors (DIR/strict_full.json)."""
 import json
 import os
 import sys
@@ -22,12 +25,15 @@ from tests import parity as P  # noqa: E402
 
 
 def main():
+    dump = sys.argv[sys.argv.index("--dump") + 1] if "--dump" in sys.argv else None
+    full = {"strict": {}, "mutations": {}}
     with np.load(os.path.join(REPO, "tests", "golden", "golden.npz")) as z:
         gold = {k: z[k] for k in z.files}
     for c in spec.COND_CASES:
         for cd in (torch.bfloat16, torch.float16):
             gpu = P.measure_strict(gold, c, cd)
             emu = P.emulated_strict(gold, c, cd)
+            full["strict"][f"{c['tag']}/{str(cd)[6:]}"] = {"gpu": gpu, "emulated": emu}
             bnd = P.strict_bounds(emu, cd)
             margin = {k: (bnd[k] / gpu[k] if gpu[k] > 0 else float("inf")) for k in gpu}
             ratio = [gpu[k] / emu[k] for k in gpu if emu[k] > 0]
@@ -47,6 +53,14 @@ def main():
                 "gpu_over_emulated": {"median": round(float(np.median(ratio)), 3),
                                       "p90": round(float(np.percentile(ratio, 90)), 3),
                                       "max": round(float(max(ratio)), 3)}}), flush=True)
+    if dump:
+        from tests import test_gpu_models as TM
+        c = [c for c in spec.COND_CASES if c["tag"] == "cond_tr_fc"][0]
+        for name, mut in TM.MUTATIONS.items():
+            full["mutations"][name] = TM._mutated_errors(gold, c, torch.bfloat16, mut)
+        os.makedirs(dump, exist_ok=True)
+        with open(os.path.join(dump, "strict_full.json"), "w") as f:
+            json.dump(full, f)
     for c in spec.TT_CASES:
         for cd in (torch.bfloat16, torch.float16):
             gpu = P.run_stats(P.measure(gold, c, cd))

@@ -33,14 +33,16 @@ def _inputs():
             torch.from_numpy(labels("dp.lv", (B, T))), torch.from_numpy(labels("dp.la", (B, T))))
 
 
-def _model(hashed=True):
+def _model(hashed=True, jm="TRANSFORMER"):
     """hashed: the discriminative counter-hash init of the goldens (sharp attention: 16-bit runs
     of it differ by O(10 %) in the gradients from any reordering, tests/parity.py); otherwise
-    torch's default init under a fixed seed (smooth: 16-bit differences stay O(1e-3))."""
+    torch's default init under a fixed seed (smooth: 16-bit differences stay O(1e-3)).
+    jm: joint_modalities ("NONE" = MultimodalTransformer_wo_JR, bench config c2, whose encoder
+    and cross-attention backwards run on the run_parallel branch streams)."""
     from models.two_transformers import Two_transformers
     from oracle.hashinit import init_module_
     torch.manual_seed(0)
-    m = Two_transformers(0.0, 0.0, 1, 1, "TRANSFORMER", "FC", VIN)
+    m = Two_transformers(0.0, 0.0, 1, 1, jm, "FC", VIN)
     if hashed:
         init_module_(m, "")
     return m
@@ -104,18 +106,17 @@ def _train_step_worker(rank, world, port, q, cd_name):
         dist.destroy_process_group()
 
 
-def _dp_oracle():
+def _dp_oracle(jm="TRANSFORMER"):
     """nn.DataParallel on 2 replicas, restated on the CPU oracle: per-replica forward on the
     dim-0 shard, outputs gathered on dim 0, CCC on the gathered (1, B*T) view, grads."""
     from oracle import jmt_ref as R
-    m = _model()
+    m = _model(jm=jm)
     p = {k: v.detach().clone().float().requires_grad_(True) for k, v in m.state_dict().items()}
     audio, video, lv, la = _inputs()
     vos, aos = [], []
     for r in range(2):
         sl = slice(r * B // 2, (r + 1) * B // 2)
-        vo, ao = R.two_transformers_forward(audio[sl], video[sl], p, 1, 1, "TRANSFORMER", "FC",
-                                            VIN)
+        vo, ao = R.two_transformers_forward(audio[sl], video[sl], p, 1, 1, jm, "FC", VIN)
         vos.append(vo)
         aos.append(ao)
     vo, ao = torch.cat(vos, 0), torch.cat(aos, 0)
@@ -234,17 +235,20 @@ def test_two_rank_losses_unequal_shards_match_gathered_batch(kind):
         off += SIZES[rank]
 
 
-def _bucketed_worker(rank, world, port, q):
+def _bucketed_worker(rank, world, port, q, jm="TRANSFORMER", side=True):
     """bench.py's N>1 step: FusedSGD's flat gradients in write-completion order and the
-    all-reduce issued bucket by bucket during the backward (jmt.dist.GradBucketer)."""
+    all-reduce issued bucket by bucket during the backward (jmt.dist.GradBucketer).  side=False
+    turns the weight-gradient side stream off (JMT_SIDE_STREAM=0, bench.py's probe steps)."""
     dist, jdist = _init(rank, world, port)
     try:
         from jmt import functional as JF
+        from jmt import streams
         from jmt.optim import FusedSGD
         from losses.loss import CCCLoss
+        streams.set_side_enabled(side)
         audio, video, lv, la = _inputs()
         lo, hi = jdist.shard_range(B, rank, world)
-        m = _model().cuda()
+        m = _model(jm=jm).cuda()
         crit = CCCLoss(1)
         a, v = audio[lo:hi].cuda(), video[lo:hi].cuda()
         n = (hi - lo) * T
@@ -274,9 +278,14 @@ def _bucketed_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_overlapped_bucket_allreduce_matches_dataparallel_oracle():
-    out = sorted(_spawn_raw(_bucketed_worker), key=lambda r: r[0])
-    ref_loss, ref_grads = _dp_oracle()
+@pytest.mark.parametrize("jm,side", [("TRANSFORMER", True), ("NONE", True),
+                                     ("TRANSFORMER", False)])
+def test_two_rank_overlapped_bucket_allreduce_matches_dataparallel_oracle(jm, side):
+    """the bucket gating must cover gradient writes on every stream —
+    the grouped w_JR model (side stream on / off) and the wo_JR model (c2), whose branch
+    backwards run on the run_parallel streams."""
+    out = sorted(_spawn_raw(_bucketed_worker, args=(jm, side)), key=lambda r: r[0])
+    ref_loss, ref_grads = _dp_oracle(jm)
     gmax = max(float(g.abs().max()) for g in ref_grads.values())
     (_, l0, g0, early0, nb), (_, l1, g1, _, _) = out
     assert nb > 2 and early0 >= 1, (nb, early0)   # several buckets, some issued mid-backward
@@ -289,11 +298,11 @@ def test_two_rank_overlapped_bucket_allreduce_matches_dataparallel_oracle():
         assert err <= 1e-4 * max(float(r.abs().max()), 0.01 * gmax), (k, err)
 
 
-def _spawn_raw(target, world=2):
+def _spawn_raw(target, world=2, args=()):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
     for p in procs:
         p.start()
     try:
