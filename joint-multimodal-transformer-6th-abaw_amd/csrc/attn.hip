@@ -340,7 +340,10 @@ struct AttnBwdArgs {
 };
 
 // OPT: as attn_fwd_kernel (1 permlane reductions of Delta, 2 s_setprio(1) for waves 4-7, 4 the
-// next tile's K / V LDS-DMA issued in pieces between the score / dP MFMA batches)
+// next tile's K / V LDS-DMA issued in pieces between the score / dP MFMA batches); 16 each
+// tile's P / dS row stores deferred to the start of the next tile: the end-of-tile
+// vmcnt(0) that waits for the next tile's DMA otherwise also waits for the acknowledgement of
+// the stores issued just before it (stores count in vmcnt, in issue order)
 template <typename T, int OPT = 0>
 __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
   typedef typename Frag16<T>::t F;
@@ -441,9 +444,22 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
     }
     lds_barrier();                                  // Delta parts read: exchange slots free
 
+    uint2 pend[2];                                  // OPT & 16: the previous tile's P / dS
+    int pend_key[2] = {0, 0};
+    bool pend_on = false;
+    auto flush = [&]() {
+      if (pend_on) {
+        T* rowp = h == 0 ? prow_p : prow_ds;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+          if (qr < p.Lq && pend_key[kt] < p.ldp) *(uint2*)(rowp + pend_key[kt]) = pend[kt];
+        pend_on = false;
+      }
+    };
     for (int j = 0; j < nkt; ++j) {
       const char* kimg = smem + buf * 2 * IMG;
       const char* vimg = kimg + IMG;
+      if constexpr ((OPT & 16) != 0) flush();       // older than this tile's DMA
       char* nk = smem + (buf ^ 1) * 2 * IMG;        // tile j+1 (or the next item's tile 0)
       const bool stage_n = j + 1 < nkt || more;
       const T* kbn = j + 1 < nkt ? kb : kb2;
@@ -530,11 +546,15 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
         }
         const int key = kbase + 16 * kt;
         JMT_DCHECK(qc >= 0 && qc < p.Lq && item < p.nitems);
-        if (qr < p.Lq && key < p.ldp) {
+        if constexpr ((OPT & 16) != 0) {
+          pend[kt] = h == 0 ? *(const uint2*)pv4 : *(const uint2*)ds4;
+          pend_key[kt] = key;
+        } else if (qr < p.Lq && key < p.ldp) {
           if (h == 0) *(uint2*)(prow_p + key) = *(const uint2*)pv4;
           else *(uint2*)(prow_ds + key) = *(const uint2*)ds4;
         }
       }
+      if constexpr ((OPT & 16) != 0) pend_on = true;
       // ---- acc[t] += sum_k dS(k) K[k][256h + 16t + 4g + r] (transposed K fragments in
       // double-buffered batches of 4)
       {
@@ -570,6 +590,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
       }
       buf ^= 1;
     }
+    if constexpr ((OPT & 16) != 0) flush();         // the item's last tile
     store_acc_direct<T>(acc, 1.f,
                         (T*)p.dq + (int64_t)n * p.sdq_n + hd * AT_DH + (int64_t)qr * p.sdq_l +
                             256 * h,
@@ -685,7 +706,7 @@ extern "C" int jmt_attn_fwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
     (void)once;
     hipLaunchKernelGGL((attn_fwd_kernel<__bf16, true>), grid, dim3(512), (size_t)AF_LDS, st, a);
   } else if (dt == JMT_BF16) {
-    switch (attn_opt()) {
+    switch (attn_opt() & 15) {                      // bits 1, 2, 4, 8
       case 1: launch_fwd_bf16<1>(grid, st, a); break;
       case 2: launch_fwd_bf16<2>(grid, st, a); break;
       case 4: launch_fwd_bf16<4>(grid, st, a); break;
@@ -734,11 +755,13 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
   const dim3 grid(persistent_grid(a.nitems));
   hipStream_t st = as_stream(stream);
   if (dt == JMT_BF16) {
-    switch (attn_opt()) {
+    switch (attn_opt() & 23) {                      // bits 1, 2, 4, 16
       case 1: launch_bwd_bf16<1>(grid, st, a); break;
       case 2: launch_bwd_bf16<2>(grid, st, a); break;
       case 4: launch_bwd_bf16<4>(grid, st, a); break;
-      case 7: case 15: launch_bwd_bf16<7>(grid, st, a); break;
+      case 7: launch_bwd_bf16<7>(grid, st, a); break;
+      case 16: launch_bwd_bf16<16>(grid, st, a); break;
+      case 23: launch_bwd_bf16<23>(grid, st, a); break;
       default: launch_bwd_bf16<0>(grid, st, a); break;
     }
   } else {

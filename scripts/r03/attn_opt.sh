@@ -9,7 +9,7 @@ JMT_ATTN_OPT=7 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -
 rc=$?; tail -2 $OUT/attn_opt_tests.log; [ $rc -ne 0 ] && exit $rc
 : > $OUT/attn_opt.jsonl
 for round in 1 2; do
-  for o in ${OPTS:-0 1 2 4 8 7 15}; do
+  for o in ${OPTS:-0 1 2 4 8 16 7 15 31}; do
     for shape in "384 300 40" "192 300 40"; do
       r=$(JMT_ATTN_OPT=$o timeout -k 10 120 python scripts/bench_attn.py $shape) || exit 1
       echo "{\"opt\": $o, \"round\": $round, \"r\": $r}" | tee -a $OUT/attn_opt.jsonl
