@@ -627,16 +627,21 @@ using namespace jmt;
 
 static void* g_stamps = nullptr;
 
-// JMT_ATTN_OPT (development A/B switch, read once): the OPT bits of the bf16 kernels; the fp16
-// kernels always use the default
-constexpr int ATTN_OPT_DEFAULT = 0;
-static int attn_opt() {
+// JMT_ATTN_OPT (development A/B switch, read once): the OPT bits of the bf16 kernels (forward:
+// bits 1, 2, 4, 8; backward: 1, 2, 4, 16).  Defaults = the measured-fastest combination
+// (profiles/r03_attn_opt_ab.jsonl, interleaved A/B at the c3 launches: forward 1|2|8, backward
+// 1|2|4; the fp16 kernels use the same).
+constexpr int ATTN_FWD_OPT = 11;
+constexpr int ATTN_BWD_OPT = 7;
+static int attn_opt_env() {
   static int v = [] {
     const char* e = getenv("JMT_ATTN_OPT");
-    return e ? atoi(e) : ATTN_OPT_DEFAULT;
+    return e ? atoi(e) : -1;
   }();
   return v;
 }
+static int attn_opt_fwd() { return attn_opt_env() < 0 ? ATTN_FWD_OPT : (attn_opt_env() & 15); }
+static int attn_opt_bwd() { return attn_opt_env() < 0 ? ATTN_BWD_OPT : (attn_opt_env() & 23); }
 
 template <int OPT>
 static void launch_fwd_bf16(dim3 grid, hipStream_t st, const AttnFwdArgs& a) {
@@ -706,19 +711,18 @@ extern "C" int jmt_attn_fwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
     (void)once;
     hipLaunchKernelGGL((attn_fwd_kernel<__bf16, true>), grid, dim3(512), (size_t)AF_LDS, st, a);
   } else if (dt == JMT_BF16) {
-    switch (attn_opt() & 15) {                      // bits 1, 2, 4, 8
+    switch (attn_opt_fwd()) {
+      case 0: launch_fwd_bf16<0>(grid, st, a); break;
       case 1: launch_fwd_bf16<1>(grid, st, a); break;
       case 2: launch_fwd_bf16<2>(grid, st, a); break;
       case 4: launch_fwd_bf16<4>(grid, st, a); break;
-      case 7: launch_fwd_bf16<7>(grid, st, a); break;
       case 8: launch_fwd_bf16<8>(grid, st, a); break;
-      case 15: launch_fwd_bf16<15>(grid, st, a); break;
-      default: launch_fwd_bf16<0>(grid, st, a); break;
+      default: launch_fwd_bf16<ATTN_FWD_OPT>(grid, st, a); break;
     }
   } else {
-    static bool once = (set_lds(attn_fwd_kernel<_Float16, false, ATTN_OPT_DEFAULT>, AF_LDS), true);
+    static bool once = (set_lds(attn_fwd_kernel<_Float16, false, ATTN_FWD_OPT>, AF_LDS), true);
     (void)once;
-    hipLaunchKernelGGL((attn_fwd_kernel<_Float16, false, ATTN_OPT_DEFAULT>), grid, dim3(512),
+    hipLaunchKernelGGL((attn_fwd_kernel<_Float16, false, ATTN_FWD_OPT>), grid, dim3(512),
                        (size_t)AF_LDS, st, a);
   }
   JMT_LAUNCH_CHECK("jmt_attn_fwd");
@@ -755,19 +759,16 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
   const dim3 grid(persistent_grid(a.nitems));
   hipStream_t st = as_stream(stream);
   if (dt == JMT_BF16) {
-    switch (attn_opt() & 23) {                      // bits 1, 2, 4, 16
-      case 1: launch_bwd_bf16<1>(grid, st, a); break;
-      case 2: launch_bwd_bf16<2>(grid, st, a); break;
-      case 4: launch_bwd_bf16<4>(grid, st, a); break;
-      case 7: launch_bwd_bf16<7>(grid, st, a); break;
+    switch (attn_opt_bwd()) {
+      case 0: launch_bwd_bf16<0>(grid, st, a); break;
       case 16: launch_bwd_bf16<16>(grid, st, a); break;
       case 23: launch_bwd_bf16<23>(grid, st, a); break;
-      default: launch_bwd_bf16<0>(grid, st, a); break;
+      default: launch_bwd_bf16<ATTN_BWD_OPT>(grid, st, a); break;
     }
   } else {
-    static bool once = (set_lds(attn_bwd_kernel<_Float16, ATTN_OPT_DEFAULT>, AB_LDS), true);
+    static bool once = (set_lds(attn_bwd_kernel<_Float16, ATTN_BWD_OPT>, AB_LDS), true);
     (void)once;
-    hipLaunchKernelGGL((attn_bwd_kernel<_Float16, ATTN_OPT_DEFAULT>), grid, dim3(512),
+    hipLaunchKernelGGL((attn_bwd_kernel<_Float16, ATTN_BWD_OPT>), grid, dim3(512),
                        (size_t)AB_LDS, st, a);
   }
   JMT_LAUNCH_CHECK("jmt_attn_bwd");

@@ -130,12 +130,17 @@ def emulated(golden: dict, c: dict, cd) -> dict:
 
 
 # ---- STRICT 16-bit suite (round 3; spec.COND_CASES, tests/test_gpu_models.py) ----------------
-# bound(q) = min(CEIL[kind], K_STRICT x max(emulated error of q, 2u)): the HIP run may be at most
-# K_STRICT times as far from the fp32 reference as the rounding-emulating oracle on the SAME
+# bound(q) = min(CEIL[kind], K_STRICT x max(emulated error of q, floor)): the HIP run may be at
+# most K_STRICT times as far from the fp32 reference as the rounding-emulating oracle on the SAME
 # quantity (no group / median floors), and never beyond an absolute ceiling: 5 % (bf16) / 2 %
 # (fp16) relative on predictions, losses and every parameter gradient; 9 % / 3.5 % on the
-# recorded intermediates and their gradients (all rows) and the inputs' gradients.  Margins (bound / error) of every
-# quantity are reported by scripts/parity_report.py (profiles/r03_parity_error_model.txt).
+# recorded intermediates and their gradients (all rows) and the inputs' gradients.
+# floor: u/2 (one rounding of the stored result) for forward VALUES — predictions, losses,
+# recorded activations, whose rounding points the emulation reproduces (GPU / emulated ratio
+# 0.98-1.0) — and 2u for gradients (accumulation order differs).  A 2u floor on the values
+# (K x 2u = 3.1 % in bf16) hid a 2 % error in a cross-attention's out_proj weight
+# (profiles/r03_parity_error_model.jsonl: its CA output is then 2.03 % off against 0.39 %
+# emulated).  Margins (bound / error) of every quantity: scripts/parity_report.py.
 UNIT = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11}   # unit roundoff of 16-bit storage
 K_STRICT = 4.0
 CEIL = {torch.bfloat16: {"param": 0.05, "out": 0.05, "inter": 0.09},
@@ -250,9 +255,14 @@ def emulated_strict(golden: dict, c: dict, cd) -> dict:
                          o["taps"])
 
 
+def _is_value(q: str) -> bool:
+    return q.startswith("out:") or q.endswith(":val")
+
+
 def strict_bounds(emu: dict, cd) -> dict:
     u = UNIT[cd]
-    return {k: min(CEIL[cd][k.split(":")[0]], K_STRICT * max(e, 2 * u)) for k, e in emu.items()}
+    return {k: min(CEIL[cd][k.split(":")[0]], K_STRICT * max(e, (0.5 if _is_value(k) else 2.0) * u))
+            for k, e in emu.items()}
 
 
 def check16_strict(gpu: dict, emu: dict, cd) -> list:
