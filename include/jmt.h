@@ -169,6 +169,17 @@ int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* go, i
                  void* ds_out, int64_t ldp, void* dq, int64_t sdq_l, int64_t sdq_n, float scale,
                  void* stream);
 
+/* jmt_attn_bwd with P and dS handed over KEY-major (round 3): p_out / ds_out row
+ * (n*H + h)*Lk + k holds key k's probabilities / dS over the queries (columns [0, Lq), row stride
+ * ldt >= Lq, columns [Lq, ldt) not written), so the dK = ds^T Q and dV = P^T dO products read a
+ * K-major A operand (jmt_gemm's 160 x 256 tile applies); dq as jmt_attn_bwd. */
+int jmt_attn_bwd_km(int dt, int N, int H, int Lq, int Lk, int dh, const void* go, int64_t sgo_l,
+                    int64_t sgo_n, const void* o, int64_t so_l, int64_t so_n, const void* q,
+                    int64_t sq_l, int64_t sq_n, const void* k, int64_t sk_l, int64_t sk_n,
+                    const void* v, int64_t sv_l, int64_t sv_n, const float* lse, void* p_out,
+                    void* ds_out, int64_t ldt, void* dq, int64_t sdq_l, int64_t sdq_n,
+                    float scale, void* stream);
+
 /* Fused attention over short sequences, the whole backward in one kernel (Lq, Lk <= 32, 16-bit,
  * dh = 512; the batch-axis self-attention of mm_transformers.py:119-146 at B = 32 and every
  * attention of the T = 16 real-data configuration): same element addressing as jmt_attn_*,

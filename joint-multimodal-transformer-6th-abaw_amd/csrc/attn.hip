@@ -344,7 +344,9 @@ struct AttnBwdArgs {
 // tile's P / dS row stores deferred to the start of the next tile: the end-of-tile
 // vmcnt(0) that waits for the next tile's DMA otherwise also waits for the acknowledgement of
 // the stores issued just before it (stores count in vmcnt, in issue order)
-template <typename T, int OPT = 0>
+// KM: P and dS handed over KEY-major (rows (n H + h) Lk + key, query columns, stride ldp >= Lq) so
+// that dK = (dS^T) Q and dV = (P^T) dO read a K-major A operand (jmt_attn_bwd_km)
+template <typename T, int OPT = 0, bool KM = false>
 __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
   typedef typename Frag16<T>::t F;
   typedef typename Frag16<T>::h Hf;
@@ -546,7 +548,14 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
         }
         const int key = kbase + 16 * kt;
         JMT_DCHECK(qc >= 0 && qc < p.Lq && item < p.nitems);
-        if constexpr ((OPT & 16) != 0) {
+        if constexpr (KM) {                         // 2-B stores down the key rows
+          if (qr < p.Lq) {
+            T* col = (T*)(h == 0 ? p.pbuf : p.dsbuf) + (int64_t)nh * p.Lk * p.ldp + qr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (key + r < p.Lk) col[(int64_t)(key + r) * p.ldp] = h == 0 ? pv4[r] : ds4[r];
+          }
+        } else if constexpr ((OPT & 16) != 0) {
           pend[kt] = h == 0 ? *(const uint2*)pv4 : *(const uint2*)ds4;
           pend_key[kt] = key;
         } else if (qr < p.Lq && key < p.ldp) {
@@ -554,7 +563,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
           else *(uint2*)(prow_ds + key) = *(const uint2*)ds4;
         }
       }
-      if constexpr ((OPT & 16) != 0) pend_on = true;
+      if constexpr ((OPT & 16) != 0 && !KM) pend_on = true;
       // ---- acc[t] += sum_k dS(k) K[k][256h + 16t + 4g + r] (transposed K fragments in
       // double-buffered batches of 4)
       {
@@ -655,6 +664,13 @@ static void launch_bwd_bf16(dim3 grid, hipStream_t st, const AttnBwdArgs& a) {
   static bool once = (set_lds(attn_bwd_kernel<__bf16, OPT>, AB_LDS), true);
   (void)once;
   hipLaunchKernelGGL((attn_bwd_kernel<__bf16, OPT>), grid, dim3(512), (size_t)AB_LDS, st, a);
+}
+template <typename T>
+static void launch_bwd_km(dim3 grid, hipStream_t st, const AttnBwdArgs& a) {
+  constexpr int O = ATTN_BWD_OPT & ~16;
+  static bool once = (set_lds(attn_bwd_kernel<T, O, true>, AB_LDS), true);
+  (void)once;
+  hipLaunchKernelGGL((attn_bwd_kernel<T, O, true>), grid, dim3(512), (size_t)AB_LDS, st, a);
 }
 
 // one block per CU (the 160 KiB of LDS admit one), rounded down to a multiple of 8 (XCDs), when
@@ -772,5 +788,42 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
                        (size_t)AB_LDS, st, a);
   }
   JMT_LAUNCH_CHECK("jmt_attn_bwd");
+  return JMT_OK;
+}
+
+// P / dS handed over key-major: p_out / ds_out rows (n*H + h)*Lk + key, columns = queries, row
+// stride ldt >= Lq (include/jmt.h); everything else as jmt_attn_bwd
+extern "C" int jmt_attn_bwd_km(int dt, int N, int H, int Lq, int Lk, int dh, const void* go,
+                               int64_t sgo_l, int64_t sgo_n, const void* o, int64_t so_l,
+                               int64_t so_n, const void* q, int64_t sq_l, int64_t sq_n,
+                               const void* k, int64_t sk_l, int64_t sk_n, const void* v,
+                               int64_t sv_l, int64_t sv_n, const float* lse, void* p_out,
+                               void* ds_out, int64_t ldt, void* dq, int64_t sdq_l, int64_t sdq_n,
+                               float scale, void* stream) {
+  if (N == 0 || Lq == 0) return JMT_OK;
+  if (!jmt_attn_supported(dt, dh))
+    return set_error(JMT_ERR_UNSUPPORTED, "jmt_attn_bwd_km: dtype %d / head dim %d not supported",
+                     dt, dh);
+  const void* ptrs[] = {go, o, q, k, v, p_out, ds_out, dq};
+  const int64_t strides[] = {sgo_l, sgo_n, so_l, so_n, sq_l, sq_n, sk_l, sk_n, sv_l, sv_n,
+                             sdq_l, sdq_n, ldt};
+  int rc = check_common("jmt_attn_bwd_km", N, H, Lq, Lk, ptrs, 8, strides, 13);
+  if (rc != JMT_OK) return rc;
+  JMT_CHECK_ARG(lse && ldt >= Lq, "jmt_attn_bwd_km: lse missing or ldt < Lq");
+  AttnBwdArgs a = {};
+  a.go = go; a.o = o; a.q = q; a.k = k; a.v = v; a.lse = lse;
+  a.pbuf = p_out; a.dsbuf = ds_out; a.dq = dq;
+  a.sgo_l = sgo_l; a.sgo_n = sgo_n; a.so_l = so_l; a.so_n = so_n; a.sq_l = sq_l; a.sq_n = sq_n;
+  a.sk_l = sk_l; a.sk_n = sk_n; a.sv_l = sv_l; a.sv_n = sv_n; a.sdq_l = sdq_l; a.sdq_n = sdq_n;
+  a.ldp = ldt;
+  a.Lq = Lq; a.Lk = Lk; a.H = H;
+  a.scale = scale;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.nitems = ((Lq + AT_QT - 1) / AT_QT) * N * H;
+  const dim3 grid(persistent_grid(a.nitems));
+  hipStream_t st = as_stream(stream);
+  if (dt == JMT_BF16) launch_bwd_km<__bf16>(grid, st, a);
+  else launch_bwd_km<_Float16>(grid, st, a);
+  JMT_LAUNCH_CHECK("jmt_attn_bwd_km");
   return JMT_OK;
 }

@@ -87,6 +87,10 @@ _PROTOS = {
                                    c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
                                    c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
                                    c_i64, c_vp, c_i64, c_i64, c_f, c_vp]),
+    "jmt_attn_bwd_km": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
+                                c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
+                                c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_f,
+                                c_vp]),
     "jmt_noop": (c_int, [c_vp]),
     "jmt_small_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
                                    c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,

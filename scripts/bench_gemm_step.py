@@ -37,6 +37,10 @@ def make_shapes(R):
         ("regressor dgrad NN 1024x128 beta", R, 1024, 128, True, False, 1, BF16, {"beta": 1.0}),
         ("regressor fwd pair NT 128x1024 relu", R, 128, 1024, True, True, 2, BF16, {"sA0": True}),
         ("attn dKdV b384 TN 300x512x320 (K padded)", 300, 512, 320, False, False, 384, BF16, {}),
+        # round 3: P^T / dS^T handed over key-major (K-major A), so the 160-row tile applies
+        ("attn dKdV b384 NN 300x512x300 (dS^T K-major)", 300, 512, 300, True, False, 384, BF16, {}),
+        ("attn dKdV b192 NN 300x512x300 (dS^T K-major)", 300, 512, 300, True, False, 192, BF16, {}),
+        ("attn dKdV b192 TN 300x512x300", 300, 512, 300, False, False, 192, BF16, {}),
         ("attn dKdV b384 TN 320x512x320 (M, K padded)", 320, 512, 320, False, False, 384, BF16, {}),
         ("attn dKdV b768 TN 300x512x300 (dK + dV)", 300, 512, 300, False, False, 768, BF16, {}),
         ("attn dKdV b768 TN 300x512x320 (dK + dV, K padded)", 300, 512, 320, False, False, 768, BF16, {}),

@@ -775,3 +775,41 @@ def test_head_kernels_vs_torch(k, dt):
         rb = 1.0 + G.sum(0)
         assert (db[i] - rb).abs().max().item() <= 1e-4 * max(1.0, rb.abs().max().item())
     assert torch.isnan(dh[:, 256:].float()).all(), "wrote past the two heads"
+
+
+@pytest.mark.parametrize("Lq,Lk,N", [(300, 300, 5), (70, 129, 3), (129, 1, 2), (33, 300, 4)])
+def test_fused_attention_bwd_keymajor_handoff(Lq, Lk, N):
+    """jmt_attn_bwd_km writes the same P and dS as jmt_attn_bwd, key-major (rows = keys, columns
+    = queries, stride ldt), and the same dq bit for bit; padding columns are never written."""
+    cd = torch.bfloat16
+    E = 512
+    g = torch.Generator(device=DEV).manual_seed(29)
+    qkv = torch.randn(N, Lq, 3 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    kv = torch.randn(N, Lk, 2 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    qp, kp, vp = qkv[..., :E], kv[..., :E], kv[..., E:]
+    scale = 1.0 / math.sqrt(E)
+    dt = ops.dt(qkv)
+    st = lambda t: (t.stride(0), t.stride(1))
+    o = torch.empty(Lq, N, E, device=DEV, dtype=cd)
+    lse = torch.empty(N * Lq, device=DEV, dtype=torch.float32)
+    ops.attn_fwd(dt, N, 1, Lq, Lk, E, qp.data_ptr(), st(qkv), kp.data_ptr(), st(kv),
+                 vp.data_ptr(), st(kv), o.data_ptr(), st(o), scale, lse)
+    go = torch.randn(Lq, N, E, device=DEV, generator=g).to(cd)
+    ldp, ldt = _rup(Lk, 8), _rup(Lq, 8) + 8
+    P = torch.empty(N * Lq * ldp, device=DEV, dtype=cd)
+    dS = torch.empty_like(P)
+    dq = torch.empty(Lq, N, E, device=DEV, dtype=cd)
+    args = (go.data_ptr(), st(go), o.data_ptr(), st(o), qp.data_ptr(), st(qkv), kp.data_ptr(),
+            st(kv), vp.data_ptr(), st(kv), lse)
+    ops.attn_bwd(dt, N, 1, Lq, Lk, E, *args, P, dS, ldp, dq.data_ptr(), st(dq), scale)
+    Pt = torch.full((N * Lk * ldt,), float("nan"), device=DEV, dtype=cd)
+    dSt = torch.full_like(Pt, float("nan"))
+    dq2 = torch.empty_like(dq)
+    ops.attn_bwd_km(dt, N, 1, Lq, Lk, E, *args, Pt, dSt, ldt, dq2.data_ptr(), st(dq2), scale)
+    torch.cuda.synchronize()
+    assert torch.equal(dq, dq2)
+    Pk = Pt.view(N, Lk, ldt)
+    dSk = dSt.view(N, Lk, ldt)
+    assert torch.equal(Pk[..., :Lq], P.view(N, Lq, ldp)[..., :Lk].transpose(1, 2))
+    assert torch.equal(dSk[..., :Lq], dS.view(N, Lq, ldp)[..., :Lk].transpose(1, 2))
+    assert torch.isnan(Pk[..., Lq:].float()).all() and torch.isnan(dSk[..., Lq:].float()).all()
