@@ -9,7 +9,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; tail $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
-timeout -k 10 400 python bench.py > $OUT/bench_plain.log 2>&1 || { echo bench failed; tail $OUT/bench_plain.log; exit 1; }
+timeout -k 10 400 python bench.py --launch-log $OUT/launch_log.jsonl > $OUT/bench_plain.log 2>&1 || { echo bench failed; tail $OUT/bench_plain.log; exit 1; }
 grep '^{' $OUT/bench_plain.log | tail -1 | cut -c1-300
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format rocpd csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline > $OUT/bench_prof.log 2>&1 || { echo prof failed; tail $OUT/bench_prof.log; exit 1; }
 db=$(find $OUT/prof -name "*results.db" | head -1)
