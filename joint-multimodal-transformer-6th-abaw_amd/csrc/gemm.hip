@@ -1094,6 +1094,9 @@ static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, in
   if (splits <= 1 && ak && M >= 4096 && K >= 512 && K % 64 == 0 &&
       ((batch == 1 && N <= 1024) || (bk && batch == 3 && N == 1536 && K == 512)))
     return 30;
+  // the stacked-stream dgrad of out_layer_pv (b2, beta = 1): 65 -> 57 us (1.17 waves of 256x256
+  // tiles, 1.88 of 160x256; profiles/r03_nn_sweep.jsonl)
+  if (splits <= 1 && ak && !bk && batch == 2 && M >= 4096 && N == 512 && K == 512) return 30;
   if (!ak && !bk && M >= 1536 && N >= 512 && batch >= 3 && K >= 8192)
     return 10;                                                   // split-K qkv wgrad
   if (!ak && !bk && batch == 6 && M == 1024 && N == 512 && K >= 8192)

@@ -183,18 +183,24 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
   }
 }
 
-// fixed-order sum of the blocks' slabs into the gradient buffers (+=)
+// fixed-order sum of the blocks' slabs into the gradient buffers (+=): one wave per output
+// (wave-uniform index), lane l adds slabs l, l + 64, ... in order, then a fixed xor butterfly;
+// lane 0 stores.  (One thread per output walking all ~300 slabs serially was a 74 us chain of
+// dependent L2 loads per step: profiles/r03_p1_kernel_stats.csv.)
 __global__ __launch_bounds__(256) void head_reduce_kernel(HeadArgs a, int nblk) {
   const int SK = a.k * (HD_HID + 1);
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (i >= 2 * SK) return;
   const int g = i / SK, j = i % SK;
   const bool isw = j < a.k * HD_HID;
   float* dst = isw ? a.dw2[g] : a.db2[g];
   if (!dst) return;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += a.partials[(int64_t)b * 2 * SK + i];
-  dst[isw ? j : j - a.k * HD_HID] += s;
+  for (int b = lane; b < nblk; b += 64) s += a.partials[(int64_t)b * 2 * SK + i];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) dst[isw ? j : j - a.k * HD_HID] += s;
 }
 
 static int head_blocks(int64_t rows) { return (int)((rows + 4 * HD_RPW - 1) / (4 * HD_RPW)); }
@@ -278,7 +284,7 @@ extern "C" int jmt_head_bwd(int h_dt, int gy_dt, int64_t rows, int hid, int k, c
   JMT_LAUNCH_CHECK("jmt_head_bwd");
   if (dw2_0 || dw2_1 || db2_0 || db2_1) {
     const int SK = k * (HD_HID + 1);
-    hipLaunchKernelGGL(head_reduce_kernel, dim3((2 * SK + 255) / 256), dim3(256), 0, st, a, nblk);
+    hipLaunchKernelGGL(head_reduce_kernel, dim3((2 * SK + 3) / 4), dim3(256), 0, st, a, nblk);
     JMT_LAUNCH_CHECK("jmt_head_bwd(reduce)");
   }
   return JMT_OK;

@@ -26,6 +26,8 @@ def make_shapes(R):
         ("enc b3 dgrad NN aux", R, 512, 512, True, False, 3, BF16, {"aux": True}),
         ("enc b3 dgrad NN K1536 beta", R, 512, 1536, True, False, 3, BF16, {"beta": 1.0}),
         ("ca b6 dgrad NN 512x512", R, 512, 512, True, False, 6, BF16, {}),
+        ("stack b2 dgrad NN 512x512 beta", R, 512, 512, True, False, 2, BF16, {"beta": 1.0}),
+        ("ca b6 dgrad NN 512x1024", R, 512, 1024, True, False, 6, BF16, {}),
         ("ca b6 kv NT 1024x512", R, 1024, 512, True, True, 6, BF16, {}),
         ("stream dgrad kcat6 NN 512x3072", R, 512, 3072, True, False, 1, BF16, {"kcat": 6}),
         ("head dgrad b6 NN 512x1024", R, 512, 1024, True, False, 6, BF16, {"sA0": True}),

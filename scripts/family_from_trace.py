@@ -38,6 +38,10 @@ def family(name: str):
         return "small_attn_fwd"
     if "small_attn_bwd" in name:
         return "small_attn_bwd"
+    if "attn_short_fwd" in name:
+        return "attn_short_fwd"
+    if "attn_short_bwd" in name:
+        return "attn_short_bwd"
     if "attn_fwd_kernel" in name:
         return "attn_fwd"
     if "attn_bwd_kernel" in name:
