@@ -321,11 +321,16 @@ class EncoderGroupFn(Function):
     """G post-LN encoder layers (mm_multi_transformers.py:61-70, one per stream, same shapes,
     own weights) on the stacked seq-first input X (G, B, T, E):
         Y_g = LN2(H_g + W2 relu(W1 H_g + b1) + b2),  H_g = LN1(X_g + MHA_g(X_g, X_g, X_g)).
-    params: 12 per group (encoder_layer_params)."""
+    params: 12 per group (encoder_layer_params).
+    batch_axis: the self-attention runs over the B axis of each group (sequences of length B,
+    one per t) — MultimodalTransformer_wo_JR feeds its encoders batch-first tensors
+    (mm_transformers.py:119-122); the attention core is then one launch per group (a group's
+    (B, T) rows are a (seq, batch)-strided layout, the G groups together are not), every GEMM,
+    LayerNorm and bias reduction stays one grouped launch."""
 
     @staticmethod
     def forward(ctx, X, meta, *params):
-        H, eps1, eps2 = meta
+        H, eps1, eps2, batch_axis = meta
         cd = compute_dtype()
         X = _contig(X, cd)
         G, B, T, E = X.shape
@@ -338,12 +343,20 @@ class EncoderGroupFn(Function):
         QKV = torch.empty(G, B, T, 3 * E, dtype=cd, device=dev)
         _gemm_fwd([X.data_ptr()], E, R * E, R, E, [p[0] for p in P], 0, 3 * E,
                   [p[1] for p in P], QKV.data_ptr(), 3 * E, R * 3 * E, cdt, cd, dev)
-        sf = QKV.view(G * B, T, 3 * E).permute(1, 0, 2)          # (T, G*B, 3E) seq-first
-        o, asaved = attn_forward(sf, sf, sf, E, H, 0, E, 2 * E)  # memory (G*B, T, E)
-        O = o.permute(1, 0, 2)
+        if batch_axis:
+            # QKV[g] (B, T, 3E) read as seq-first (L = B, N = T): attention over the batch axis
+            outs = [attn_forward(QKV[g], QKV[g], QKV[g], E, H, 0, E, 2 * E) for g in range(G)]
+            O = [o for o, _ in outs]                           # G x (B, T, E)
+            asaved = [sv for _, sv in outs]
+            o_ptrs = [o.data_ptr() for o in O]
+        else:
+            sf = QKV.view(G * B, T, 3 * E).permute(1, 0, 2)      # (T, G*B, 3E) seq-first
+            o, asaved = attn_forward(sf, sf, sf, E, H, 0, E, 2 * E)  # memory (G*B, T, E)
+            O = o.permute(1, 0, 2)
+            o_ptrs = [O.data_ptr()]
         A1 = torch.empty(G, B, T, E, dtype=cd, device=dev)
-        _gemm_fwd([O.data_ptr()], E, R * E, R, E, [p[2] for p in P], 0, E, [p[3] for p in P],
-                  A1.data_ptr(), E, R * E, cdt, cd, dev)
+        _gemm_fwd(o_ptrs, E, R * E if len(o_ptrs) == 1 else 0, R, E, [p[2] for p in P], 0, E,
+                  [p[3] for p in P], A1.data_ptr(), E, R * E, cdt, cd, dev)
         H1 = torch.empty_like(A1)
         st1 = torch.empty(2, G * R, dtype=torch.float32, device=dev)
         for g in range(G):
@@ -362,13 +375,15 @@ class EncoderGroupFn(Function):
                               st2[0, g * R:], st2[1, g * R:], R, E)
         ctx.params = params
         ctx.state = (X, QKV, asaved, O, A1, H1, st1, F1, F2, st2)
-        ctx.meta = (G, B, T, E, hid, cd)
+        ctx.meta = (G, B, T, E, hid, cd, batch_axis)
         return Y
 
     @staticmethod
     def backward(ctx, dY):
-        G, B, T, E, hid, cd = ctx.meta
+        G, B, T, E, hid, cd, batch_axis = ctx.meta
         X, QKV, asaved, O, A1, H1, st1, F1, F2, st2 = ctx.state
+        o_ptrs = [o.data_ptr() for o in O] if batch_axis else [O.data_ptr()]
+        o_reads = tuple(O) if batch_axis else (O,)
         params = ctx.params
         P = [params[12 * g:12 * g + 12] for g in range(G)]
         R = B * T
@@ -447,17 +462,21 @@ class EncoderGroupFn(Function):
                     R * E, cdt, cd, dev)
 
         def out_proj_grads():   # side stream, under the attention backward
-            _gemm_wgrad([dS1.data_ptr()], E, R * E, [O.data_ptr()], E, R * E, R, E,
-                        [p[2] for p in P], 0, cd, dev)
+            _gemm_wgrad([dS1.data_ptr()], E, R * E, o_ptrs, E, R * E if len(o_ptrs) == 1 else 0,
+                        R, E, [p[2] for p in P], 0, cd, dev)
             if not bo_done:
                 _bias_grad_grouped(dS1.data_ptr(), G, E, R * E, R, E, [p[3] for p in P], 0, cd,
                                    dev)
 
-        streams.run_side(out_proj_grads, reads=(dS1, O))
+        streams.run_side(out_proj_grads, reads=(dS1,) + o_reads)
         # attention core -> packed dQKV
         dQKV = torch.empty(G, B, T, 3 * E, dtype=cd, device=dev)
-        dsf = dQKV.view(G * B, T, 3 * E).permute(1, 0, 2)
-        attn_backward(asaved, dO.view(G * B, T, E).permute(1, 0, 2), dsf, dsf, dsf)
+        if batch_axis:
+            for g in range(G):
+                attn_backward(asaved[g], dO[g], dQKV[g], dQKV[g], dQKV[g])
+        else:
+            dsf = dQKV.view(G * B, T, 3 * E).permute(1, 0, 2)
+            attn_backward(asaved, dO.view(G * B, T, E).permute(1, 0, 2), dsf, dsf, dsf)
         # in_proj: dX = dS1 + dQKV . W_in  (in place on dS1, once the side stream has read it)
         streams.wait_side()
         _gemm_dgrad(dQKV.data_ptr(), 3 * E, R * 3 * E, R, 3 * E, [p[0] for p in P], 0,
@@ -474,11 +493,17 @@ class EncoderGroupFn(Function):
         return (dS1, None) + (None,) * len(params)
 
 
-def encoder_group(X, layers, num_heads: int):
-    """Apply `layers` (one TransformerEncoderLayer per stream) to the stacked X."""
+def encoder_group(X, layers, num_heads: int, batch_axis: bool = False):
+    """Apply `layers` (one TransformerEncoderLayer per stream) to the stacked X (attention over
+    T, or over B with batch_axis)."""
     params = [p for layer in layers for p in encoder_layer_params(layer)]
-    meta = (num_heads, layers[0].layer_norm1.eps, layers[0].layer_norm2.eps)
+    meta = (num_heads, layers[0].layer_norm1.eps, layers[0].layer_norm2.eps, bool(batch_axis))
     return EncoderGroupFn.apply(X, meta, *params)
+
+
+# the wo_JR model's two cross-attentions (mm_transformers.py:125-135): (module, query, key/value)
+# with module 0 = cross_attention_v, 1 = cross_attention_p, stream 0 = visual, 1 = physiological
+CROSS_PAIRS_WO_JR = ((0, 0, 1), (1, 1, 0))
 
 
 # ------------------------------------------------------------------------- cross attentions

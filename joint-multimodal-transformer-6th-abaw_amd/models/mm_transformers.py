@@ -5,6 +5,7 @@ from __future__ import annotations
 import torch.nn as nn
 
 from jmt import functional as F
+from jmt import grouped
 from jmt import streams
 from jmt import taps
 from jmt.nn import Linear
@@ -39,6 +40,8 @@ class MultimodalTransformer_wo_JR(nn.Module):
         self.final_layer = Linear(1024, 512)
 
     def forward(self, visual_features, physiological_features):
+        if grouped.enabled() and visual_features.shape == physiological_features.shape:
+            return self._forward_grouped(visual_features, physiological_features)
         dev = visual_features.device
         v, p = streams.run_parallel([lambda: self.visual_encoder(visual_features),
                                      lambda: self.physiological_encoder(physiological_features)],
@@ -53,3 +56,19 @@ class MultimodalTransformer_wo_JR(nn.Module):
         taps.record("ca.1", op)
         assert self.output_format == 'FC', self.output_format
         return F.linear((ov, op), self.final_layer.weight, self.final_layer.bias)
+
+    def _forward_grouped(self, visual_features, physiological_features):
+        """Same math as forward(), the two branches batched (jmt/grouped.py): the encoders of
+        both streams as one grouped layer sequence on a stacked (2, B, T, E) buffer (their
+        self-attention over the batch axis, :120-122), the two cross-attentions over T as one
+        grouped block (:125-135), final_layer on the concatenation as one K-concatenated GEMM
+        (:139-144)."""
+        X = grouped.stack_groups(visual_features, physiological_features)
+        for lv, lp in zip(self.visual_encoder.layers, self.physiological_encoder.layers):
+            X = grouped.encoder_group(X, [lv, lp], lv.attention.num_heads, batch_axis=True)
+        taps.record_stacked(["enc.visual_encoder", "enc.physiological_encoder"], X)
+        O2 = grouped.cross_attention6(X, [self.cross_attention_v, self.cross_attention_p],
+                                      self.cross_attention_v.num_heads,
+                                      pairs=grouped.CROSS_PAIRS_WO_JR)
+        taps.record_stacked(["ca.0", "ca.1"], O2)
+        return grouped.concat_linear(O2, self.final_layer.weight, self.final_layer.bias)
