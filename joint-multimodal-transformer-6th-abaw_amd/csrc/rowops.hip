@@ -167,6 +167,16 @@ __global__ __launch_bounds__(RB) void l2norm_fwd_vec_kernel(int64_t rows, const 
   if (lane == 0) inv_norm[r] = inv;
 }
 
+// Grouped LayerNorm (round 3): G same-shaped LayerNorms (the grouped encoders' LN1 / LN2, one per
+// stream, jmt/grouped.py) in one launch, group g = blockIdx.y: its rows at x + g*sx (residual
+// r + g*sr, output / input gradient + g*sy, dy + g*sdy), statistics at mean / rstd + g*rows,
+// parameters from the tables.  gridDim.y == 1 is the plain form.
+struct LnGrp {
+  int64_t sx, sr, sy, sdy;
+  const float* gamma[8];
+  const float* beta[8];
+};
+
 // Vector forward (D = 256 NV, 4-aligned rows): lane owns elements 4*(lane + 64 j) .. +3; each
 // wave normalises LNF_RPW rows, issuing all of a row's x / residual loads before its reductions.
 constexpr int LNF_RPW = 4;
@@ -175,9 +185,20 @@ __global__ __launch_bounds__(RB) void ln_fwd_vec_kernel(int64_t rows, const TI* 
                                                         const TI* rr, int64_t ldr,
                                                         const float* gamma, const float* beta,
                                                         float eps, TO* y, int64_t ldy,
-                                                        float* mean, float* rstd) {
+                                                        float* mean, float* rstd,
+                                                        LnGrp grp = LnGrp{}) {
   constexpr int D = NV * 256;
   JMT_DCHECK(ldx >= D && ldy >= D && (!rr || ldr >= D));
+  if (gridDim.y > 1) {
+    const int gi = blockIdx.y;
+    x += gi * grp.sx;
+    if (rr) rr += gi * grp.sr;
+    y += gi * grp.sy;
+    mean += gi * rows;
+    rstd += gi * rows;
+    gamma = grp.gamma[gi];
+    beta = grp.beta[gi];
+  }
   const int lane = threadIdx.x & 63;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LNF_RPW;
   float gm[NV][4], bt[NV][4];
@@ -236,10 +257,22 @@ __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* 
                                                         const TI* rr, int64_t ldr, const TG* dy,
                                                         int64_t lddy, const float* mean,
                                                         const float* rstd, const float* gamma,
-                                                        TD* dx, int64_t lddx, float* partials) {
+                                                        TD* dx, int64_t lddx, float* partials,
+                                                        LnGrp grp = LnGrp{}) {
   constexpr int D = NV * 256;
   constexpr int NS = DS ? 3 : 2;                 // slabs: dgamma, dbeta (+ column sums of dx)
   __shared__ float red[4][NS][D];
+  if (gridDim.y > 1) {
+    const int gi = blockIdx.y;
+    x += gi * grp.sx;
+    if (rr) rr += gi * grp.sr;
+    dy += gi * grp.sdy;
+    dx += gi * grp.sy;
+    mean += gi * rows;
+    rstd += gi * rows;
+    gamma = grp.gamma[gi];
+    partials += (int64_t)gi * gridDim.x * NS * D;
+  }
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   float pg[NV][4], pb[NV][4], gm[NV][4], ps[NV][4];
@@ -380,10 +413,16 @@ __global__ __launch_bounds__(RB) void slab_reduce_kernel(int nblk, int W, const 
                                                          int64_t stride, int split, float* out0,
                                                          float* out1, int beta_acc,
                                                          OutTab tab = OutTab{}, int grouped = 0,
-                                                         float* out2 = nullptr) {
+                                                         float* out2 = nullptr,
+                                                         OutTab tab1 = OutTab{},
+                                                         OutTab tab2 = OutTab{}) {
   if (grouped) {   // group g = blockIdx.y: slabs at partials + g*nblk*stride, output tab.p[g]
     partials += (int64_t)blockIdx.y * nblk * stride;
     out0 = out1 = tab.p[blockIdx.y];
+    if (grouped == 2) {   // grouped LayerNorm: dgamma / dbeta / (dsum) tables
+      out1 = tab1.p[blockIdx.y];
+      out2 = tab2.p[blockIdx.y];
+    }
   }
   __shared__ float4 red[SR_G][4];
   __shared__ float4 red2[16][4];
@@ -928,5 +967,104 @@ __global__ void noop_kernel() {}
 extern "C" int jmt_noop(void* stream) {
   hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(64), 0, as_stream(stream));
   JMT_LAUNCH_CHECK("jmt_noop");
+  return JMT_OK;
+}
+
+// ------------------------------------------------------------------ grouped LayerNorm
+// G (<= 8) same-shaped LayerNorms in one launch (+ one reduce launch in the backward): the
+// grouped encoders' LN1 / LN2 (mm_multi_transformers.py:61-70 for each stream, jmt/grouped.py).
+// Vector layouts only (D = 512 / 768 / 1024, 4-element-aligned rows); otherwise
+// JMT_ERR_UNSUPPORTED and the caller runs the groups one by one.
+static bool ln_grp_vec(int D, int64_t ld0, int64_t ld1, int64_t ld2, int64_t s0, int64_t s1,
+                       int64_t s2, const void* p0, const void* p1, const void* p2) {
+  return (D == 512 || D == 768 || D == 1024) && ld0 % 4 == 0 && ld1 % 4 == 0 && ld2 % 4 == 0 &&
+         s0 % 4 == 0 && s1 % 4 == 0 && s2 % 4 == 0 && ((uintptr_t)p0 & 15) == 0 &&
+         ((uintptr_t)p1 & 15) == 0 && ((uintptr_t)p2 & 15) == 0;
+}
+
+extern "C" int jmt_layernorm_fwd_grouped(int dt_in, int dt_out, int G, int64_t rows, int D,
+                                         const void* x, int64_t ldx, int64_t sx, const void* r,
+                                         int64_t ldr, int64_t sr, const float* const* gamma,
+                                         const float* const* beta, float eps, void* y,
+                                         int64_t ldy, int64_t sy, float* mean, float* rstd,
+                                         void* stream) {
+  if (rows == 0 || G == 0) return JMT_OK;
+  JMT_CHECK_ARG(G >= 1 && G <= 8 && gamma && beta && x && y && mean && rstd,
+                "jmt_layernorm_fwd_grouped: bad arguments");
+  if (!ln_grp_vec(D, ldx, r ? ldr : 4, ldy, sx, r ? sr : 4, sy, x, r, y))
+    return set_error(JMT_ERR_UNSUPPORTED, "jmt_layernorm_fwd_grouped: D=%d / layout", D);
+  LnGrp grp = {};
+  grp.sx = sx; grp.sr = sr; grp.sy = sy;
+  for (int g = 0; g < G; ++g) {
+    JMT_CHECK_ARG(gamma[g] && beta[g] && ((uintptr_t)gamma[g] & 15) == 0 &&
+                      ((uintptr_t)beta[g] & 15) == 0, "jmt_layernorm_fwd_grouped: gamma/beta %d", g);
+    grp.gamma[g] = gamma[g];
+    grp.beta[g] = beta[g];
+  }
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)((rows + 4 * LNF_RPW - 1) / (4 * LNF_RPW)), (unsigned)G);
+#define JMT_LNFG(NV)                                                                            \
+  hipLaunchKernelGGL((ln_fwd_vec_kernel<TI, TO, NV>), grid, dim3(RB), 0, st, rows, (const TI*)x, \
+                     ldx, (const TI*)r, ldr, grp.gamma[0], grp.beta[0], eps, (TO*)y, ldy, mean,  \
+                     rstd, grp)
+  JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_out, TO,
+      if (D == 512) { JMT_LNFG(2); }
+      else if (D == 768) { JMT_LNFG(3); }
+      else { JMT_LNFG(4); }));
+#undef JMT_LNFG
+  JMT_LAUNCH_CHECK("jmt_layernorm_fwd_grouped");
+  return JMT_OK;
+}
+
+extern "C" int jmt_layernorm_bwd_grouped(int dt_in, int dt_dy, int dt_dx, int G, int64_t rows,
+                                         int D, const void* x, int64_t ldx, int64_t sx,
+                                         const void* r, int64_t ldr, int64_t sr, const void* dy,
+                                         int64_t lddy, int64_t sdy, const float* mean,
+                                         const float* rstd, const float* const* gamma, void* dx,
+                                         int64_t lddx, int64_t sdx, float* const* dgamma,
+                                         float* const* dbeta, float* const* dsum, int beta_acc,
+                                         float* partials, void* stream) {
+  if (rows == 0 || G == 0) return JMT_OK;
+  JMT_CHECK_ARG(G >= 1 && G <= 8 && gamma && dgamma && dbeta && x && dy && dx && mean && rstd &&
+                    partials && ((uintptr_t)partials & 15) == 0,
+                "jmt_layernorm_bwd_grouped: bad arguments");
+  if (!ln_grp_vec(D, ldx, lddy, lddx, sx, sdy, sdx, x, dy, dx) ||
+      (r && (ldr % 4 != 0 || sr % 4 != 0 || ((uintptr_t)r & 15) != 0)))
+    return set_error(JMT_ERR_UNSUPPORTED, "jmt_layernorm_bwd_grouped: D=%d / layout", D);
+  LnGrp grp = {};
+  grp.sx = sx; grp.sr = sr; grp.sy = sdx; grp.sdy = sdy;
+  OutTab t0 = {}, t1 = {}, t2 = {};
+  for (int g = 0; g < G; ++g) {
+    JMT_CHECK_ARG(gamma[g] && ((uintptr_t)gamma[g] & 15) == 0 && dgamma[g] && dbeta[g] &&
+                      (!dsum || dsum[g]), "jmt_layernorm_bwd_grouped: group %d pointers", g);
+    grp.gamma[g] = gamma[g];
+    t0.p[g] = dgamma[g];
+    t1.p[g] = dbeta[g];
+    t2.p[g] = dsum ? dsum[g] : nullptr;
+  }
+  hipStream_t st = as_stream(stream);
+  const int nblk = jmt_layernorm_bwd_blocks(rows);
+  const dim3 grid((unsigned)nblk, (unsigned)G);
+#define JMT_LNBG(NV, DS)                                                                         \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV, DS>), grid, dim3(RB), 0, st, rows,     \
+                     (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd,     \
+                     grp.gamma[0], (TD*)dx, lddx, partials, grp)
+  JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_dy, TG, JMT_DISPATCH1(dt_dx, TD,
+      if (dsum) {
+        if (D == 512) { JMT_LNBG(2, true); }
+        else if (D == 768) { JMT_LNBG(3, true); }
+        else { JMT_LNBG(4, true); }
+      } else {
+        if (D == 512) { JMT_LNBG(2, false); }
+        else if (D == 768) { JMT_LNBG(3, false); }
+        else { JMT_LNBG(4, false); }
+      })));
+#undef JMT_LNBG
+  JMT_LAUNCH_CHECK("jmt_layernorm_bwd_grouped");
+  const int NS = dsum ? 3 : 2;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((NS * D + 15) / 16, G), dim3(RB), 0, st, nblk,
+                     NS * D, partials, (int64_t)NS * D, D, (float*)nullptr, (float*)nullptr,
+                     beta_acc, t0, 2, (float*)nullptr, t1, t2);
+  JMT_LAUNCH_CHECK("jmt_layernorm_bwd_grouped(reduce)");
   return JMT_OK;
 }

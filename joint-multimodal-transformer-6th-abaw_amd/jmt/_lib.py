@@ -69,6 +69,13 @@ _PROTOS = {
     "jmt_layernorm_bwd_dsum": (c_int, [c_int, c_int, c_int, c_i64, c_int, c_vp, c_i64, c_vp,
                                        c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
                                        c_vp, c_vp, c_int, c_vp, c_vp]),
+    "jmt_layernorm_fwd_grouped": (c_int, [c_int, c_int, c_int, c_i64, c_int, c_vp, c_i64, c_i64,
+                                          c_vp, c_i64, c_i64, c_vp, c_vp, c_f, c_vp, c_i64, c_i64,
+                                          c_vp, c_vp, c_vp]),
+    "jmt_layernorm_bwd_grouped": (c_int, [c_int, c_int, c_int, c_int, c_i64, c_int, c_vp, c_i64,
+                                          c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
+                                          c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_int,
+                                          c_vp, c_vp]),
     "jmt_softmax_fwd": (c_int, [c_int, c_i64, c_int, c_vp, c_i64, c_f, c_vp, c_i64, c_vp]),
     "jmt_softmax_bwd": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_i64, c_f, c_vp,
                                 c_i64, c_vp]),

@@ -359,9 +359,11 @@ class EncoderGroupFn(Function):
                   [p[3] for p in P], A1.data_ptr(), E, R * E, cdt, cd, dev)
         H1 = torch.empty_like(A1)
         st1 = torch.empty(2, G * R, dtype=torch.float32, device=dev)
-        for g in range(G):
-            ops.layernorm_fwd(X[g], E, A1[g], E, P[g][8], P[g][9], eps1, H1[g], E,
-                              st1[0, g * R:], st1[1, g * R:], R, E)
+        if not ops.layernorm_fwd_grouped(X, A1, [p[8] for p in P], [p[9] for p in P], eps1, H1,
+                                         st1[0], st1[1]):
+            for g in range(G):
+                ops.layernorm_fwd(X[g], E, A1[g], E, P[g][8], P[g][9], eps1, H1[g], E,
+                                  st1[0, g * R:], st1[1, g * R:], R, E)
         F1 = torch.empty(G, B, T, hid, dtype=cd, device=dev)
         _gemm_fwd([H1.data_ptr()], E, R * E, R, E, [p[4] for p in P], 0, hid,
                   [p[5] for p in P], F1.data_ptr(), hid, R * hid, cdt, cd, dev, relu=True)
@@ -370,9 +372,11 @@ class EncoderGroupFn(Function):
                   [p[7] for p in P], F2.data_ptr(), E, R * E, cdt, cd, dev)
         Y = torch.empty_like(A1)
         st2 = torch.empty(2, G * R, dtype=torch.float32, device=dev)
-        for g in range(G):
-            ops.layernorm_fwd(H1[g], E, F2[g], E, P[g][10], P[g][11], eps2, Y[g], E,
-                              st2[0, g * R:], st2[1, g * R:], R, E)
+        if not ops.layernorm_fwd_grouped(H1, F2, [p[10] for p in P], [p[11] for p in P], eps2, Y,
+                                         st2[0], st2[1]):
+            for g in range(G):
+                ops.layernorm_fwd(H1[g], E, F2[g], E, P[g][10], P[g][11], eps2, Y[g], E,
+                                  st2[0, g * R:], st2[1, g * R:], R, E)
         ctx.params = params
         ctx.state = (X, QKV, asaved, O, A1, H1, st1, F1, F2, st2)
         ctx.meta = (G, B, T, E, hid, cd, batch_axis)
@@ -401,6 +405,16 @@ class EncoderGroupFn(Function):
             any of the gradient buffers is missing (a frozen parameter) every output goes to a
             scratch block and the present buffers accumulate it afterwards."""
             fused = bias is not None
+            # all G groups in one launch pair when every gradient buffer exists
+            gb = [_grad_buffer(t) for t in gamma]
+            bb = [_grad_buffer(t) for t in beta]
+            sb = [_grad_buffer(t) for t in bias] if fused else []
+            if all(t is not None for t in gb + bb + sb) and ops.layernorm_bwd_grouped(
+                    x, r, dy, st[0], st[1], gamma, dx, gb, bb, sb if fused else None,
+                    True) is not None:
+                for g in range(G):
+                    _grad_done(gamma[g], beta[g], *([bias[g]] if fused else []))
+                return fused
             for g in range(G):
                 bufs = [_grad_buffer(gamma[g]), _grad_buffer(beta[g])]
                 if fused:

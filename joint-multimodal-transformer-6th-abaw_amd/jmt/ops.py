@@ -163,6 +163,50 @@ def layernorm_bwd_dsum(x, ldx, r, ldr, dy, lddy, mean, rstd, gamma, dx, lddx, dg
     return part
 
 
+def _ptr_array(ts):
+    arr = (C.c_void_p * len(ts))(*[t.data_ptr() if t is not None else None for t in ts])
+    return arr
+
+
+def layernorm_fwd_grouped(X, R, gammas, betas, eps, Y, mean, rstd):
+    """Y[g] = LayerNorm(X[g] (+ R[g])) with (gammas[g], betas[g]) for the G groups of the stacked
+    (G, rows, D) tensors in one launch; mean / rstd (G * rows).  False when the shape is not
+    covered (nothing written: the caller runs the groups one by one)."""
+    G, D = X.shape[0], X.shape[-1]
+    rows = X[0].numel() // D
+    ga, be = _ptr_array(gammas), _ptr_array(betas)
+    rc = _lib.load().jmt_layernorm_fwd_grouped(
+        dt(X), dt(Y), G, rows, D, X.data_ptr(), D, X[0].numel(),
+        R.data_ptr() if R is not None else None, D, R[0].numel() if R is not None else 0,
+        ga, be, eps, Y.data_ptr(), D, Y[0].numel(), mean.data_ptr(), rstd.data_ptr(), stream())
+    if rc == _lib.ERR_UNSUPPORTED:
+        return False
+    _lib.check(rc, "jmt_layernorm_fwd_grouped")
+    return True
+
+
+def layernorm_bwd_grouped(X, R, dY, mean, rstd, gammas, dX, dgammas, dbetas, dsums, beta_acc):
+    """Grouped jmt_layernorm_bwd(_dsum) over the stacked (G, rows, D) tensors: one launch + one
+    reduce; dsums None or a list of column-sum outputs.  Returns the partials buffer (keep it
+    alive until the launches are ordered) or None when the shape is not covered."""
+    G, D = X.shape[0], X.shape[-1]
+    rows = X[0].numel() // D
+    nblk = _lib.load().jmt_layernorm_bwd_blocks(rows)
+    ns = 3 if dsums is not None else 2
+    part = torch.empty(max(nblk, 1) * ns * D * G, dtype=torch.float32, device=X.device)
+    rc = _lib.load().jmt_layernorm_bwd_grouped(
+        dt(X), dt(dY), dt(dX), G, rows, D, X.data_ptr(), D, X[0].numel(),
+        R.data_ptr() if R is not None else None, D, R[0].numel() if R is not None else 0,
+        dY.data_ptr(), D, dY[0].numel(), mean.data_ptr(), rstd.data_ptr(), _ptr_array(gammas),
+        dX.data_ptr(), D, dX[0].numel(), _ptr_array(dgammas), _ptr_array(dbetas),
+        _ptr_array(dsums) if dsums is not None else None, int(beta_acc), part.data_ptr(),
+        stream())
+    if rc == _lib.ERR_UNSUPPORTED:
+        return None
+    _lib.check(rc, "jmt_layernorm_bwd_grouped")
+    return part
+
+
 def softmax_fwd(s, lds, rows, n, scale, p, ldp):
     _lib.call("jmt_softmax_fwd", dt(p), rows, n, s.data_ptr(), lds, scale, p.data_ptr(), ldp,
               stream())

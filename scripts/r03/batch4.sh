@@ -2,7 +2,7 @@
 # grouped wo_JR (c2): model / config / 2-rank tests, then c2 with the grouped path on and off
 set -u
 OUT=gpurun_out/r03; mkdir -p $OUT
-timeout -k 10 700 python -u -m pytest tests/test_gpu_models.py tests/test_gpu_configs.py tests/test_gpu_dist.py -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $OUT/b4_tests.log 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_models.py tests/test_gpu_configs.py tests/test_gpu_dist.py -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $OUT/b4_tests.log 2>&1
 rc=$?; tail -2 $OUT/b4_tests.log; [ $rc -ne 0 ] && exit $rc
 : > $OUT/c2_grouped_ab.jsonl
 for r in 1 2; do
@@ -17,3 +17,5 @@ PY
     tail -1 $OUT/c2_grouped_ab.jsonl | cut -c1-160
   done
 done
+timeout -k 10 200 python bench.py --steps 200 --no-cpu-baseline > $OUT/b4_c3.log 2>&1 || { tail -5 $OUT/b4_c3.log; exit 1; }
+grep '^{' $OUT/b4_c3.log | cut -c1-400

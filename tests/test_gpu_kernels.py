@@ -813,3 +813,51 @@ def test_fused_attention_bwd_keymajor_handoff(Lq, Lk, N):
     assert torch.equal(Pk[..., :Lq], P.view(N, Lq, ldp)[..., :Lk].transpose(1, 2))
     assert torch.equal(dSk[..., :Lq], dS.view(N, Lq, ldp)[..., :Lk].transpose(1, 2))
     assert torch.isnan(Pk[..., Lq:].float()).all() and torch.isnan(dSk[..., Lq:].float()).all()
+
+
+@pytest.mark.parametrize("dsum", [False, True])
+@pytest.mark.parametrize("cd", [torch.bfloat16, torch.float32])
+def test_layernorm_grouped_equals_per_group(dsum, cd):
+    """jmt_layernorm_{fwd,bwd}_grouped (G groups, one launch each + one reduce) give bitwise the
+    per-group jmt_layernorm_fwd / _bwd(_dsum) results: same kernels, same partial-sum order."""
+    G, rows, D = 3, 1900, 512
+    g = torch.Generator(device=DEV).manual_seed(37)
+    X = torch.randn(G, rows, D, device=DEV, generator=g).to(cd)
+    Rr = torch.randn(G, rows, D, device=DEV, generator=g).to(cd)
+    dY = torch.randn(G, rows, D, device=DEV, generator=g).to(cd)
+    gam = [torch.randn(D, device=DEV, generator=g) for _ in range(G)]
+    bet = [torch.randn(D, device=DEV, generator=g) for _ in range(G)]
+    Y1, Y2 = torch.empty_like(X), torch.empty_like(X)
+    st1 = torch.empty(2, G * rows, device=DEV)
+    st2 = torch.empty(2, G * rows, device=DEV)
+    for i in range(G):
+        ops.layernorm_fwd(X[i], D, Rr[i], D, gam[i], bet[i], 1e-5, Y1[i], D, st1[0, i * rows:],
+                          st1[1, i * rows:], rows, D)
+    assert ops.layernorm_fwd_grouped(X, Rr, gam, bet, 1e-5, Y2, st2[0], st2[1])
+    torch.cuda.synchronize()
+    assert torch.equal(Y1, Y2) and torch.equal(st1, st2)
+    outs = []
+    for grouped in (False, True):
+        dX = torch.empty_like(X)
+        dg = [torch.full((D,), 0.5, device=DEV) for _ in range(G)]
+        db = [torch.full((D,), 0.25, device=DEV) for _ in range(G)]
+        ds = [torch.full((D,), 1.0, device=DEV) for _ in range(G)] if dsum else None
+        if grouped:
+            assert ops.layernorm_bwd_grouped(X, Rr, dY, st1[0], st1[1], gam, dX, dg, db, ds,
+                                             True) is not None
+        else:
+            for i in range(G):
+                a = (X[i], D, Rr[i], D, dY[i], D, st1[0, i * rows:], st1[1, i * rows:], gam[i],
+                     dX[i], D, dg[i], db[i])
+                if dsum:
+                    assert ops.layernorm_bwd_dsum(*a, ds[i], True, rows, D) is not None
+                else:
+                    ops.layernorm_bwd(*a, True, rows, D)
+        torch.cuda.synchronize()
+        outs.append((dX, dg, db, ds))
+    (a, b) = outs
+    assert torch.equal(a[0], b[0])
+    for i in range(G):
+        assert torch.equal(a[1][i], b[1][i]) and torch.equal(a[2][i], b[2][i])
+        if dsum:
+            assert torch.equal(a[3][i], b[3][i])
