@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define JMT_ABI_VERSION 3
+#define JMT_ABI_VERSION 4
 
 enum { JMT_F32 = 0, JMT_BF16 = 1, JMT_F16 = 2 };
 enum { JMT_OK = 0, JMT_ERR_ARG = -1, JMT_ERR_HIP = -2, JMT_ERR_UNSUPPORTED = -3 };
@@ -80,6 +80,16 @@ typedef struct jmt_gemm_desc {
    * launch): when n_bias > 0, batch b0 uses bias_tab[b0] (bias_mode 1 or 2) instead of bias. */
   const float* bias_tab[8];
   int n_bias;
+  /* ABI 4: A row sums — the bias gradient of a weight-gradient GEMM dW = dY^T X, db[m] =
+   * sum_k A[m][k] = the column sums of dY (nn.Linear's bias.grad, autograd of the same
+   * modules) — taken from the A fragments inside the GEMM instead of a second pass over dY:
+   * when n_dbias > 0, dbias_tab[b0][m] (+)= (dbias_acc) the row sums of A[b0] (fp32).  16-bit
+   * MN-major A and B, fp32 C, batch1 = 1; split-K needs dbias_ws (splits * batch0 * M floats). */
+  float* dbias_tab[8];
+  int n_dbias;
+  int dbias_acc;
+  float* dbias_ws;
+  size_t dbias_ws_bytes;
 } jmt_gemm_desc;
 
 int jmt_gemm(const jmt_gemm_desc* desc, void* stream);

@@ -12,6 +12,15 @@
 
 static int g_fail = 0;
 
+// the error message names the check (not a later failure, e.g. a launch without a device)
+static void expect_msg(const char* what, const char* needle) {
+  const char* e = jmt_last_error();
+  if (!e || !strstr(e, needle)) {
+    fprintf(stderr, "FAIL %s: err='%s' lacks '%s'\n", what, e ? e : "(null)", needle);
+    ++g_fail;
+  }
+}
+
 static void expect_err(const char* what, int rc) {
   const char* e = jmt_last_error();
   const size_t n = e ? strnlen(e, 1024) : 0;
@@ -26,7 +35,7 @@ int main() {
     fprintf(stderr, "FAIL abi version\n");
     return 1;
   }
-  char buf[64];
+  alignas(16) char buf[64];
   float* fnull = nullptr;
   void* misal = (void*)(buf + 1);
 
@@ -45,6 +54,18 @@ int main() {
   expect_err("gemm dtype", jmt_gemm(&d, nullptr));
   d.ab_dtype = JMT_BF16; d.M = -5;
   expect_err("gemm negative M", jmt_gemm(&d, nullptr));
+  // A row sums (ABI 4): table entries, layout and table size are checked before any launch
+  d.M = 128; d.a[0] = d.b[0] = d.c[0] = (void*)buf; d.c_dtype = JMT_F32;
+  d.a_kmajor = 0; d.b_kmajor = 0; d.n_dbias = 1; d.dbias_tab[0] = nullptr;
+  expect_err("gemm dbias null entry", jmt_gemm(&d, nullptr));
+  expect_msg("gemm dbias null entry", "dbias_tab");
+  d.dbias_tab[0] = (float*)buf; d.a_kmajor = 1;
+  expect_err("gemm dbias K-major A", jmt_gemm(&d, nullptr));
+  expect_msg("gemm dbias K-major A", "row sums");
+  d.a_kmajor = 0; d.n_dbias = 9;
+  expect_err("gemm dbias table > 8", jmt_gemm(&d, nullptr));
+  expect_msg("gemm dbias table > 8", "dbias table");
+  d.n_dbias = 0;
   expect_err("gemm null desc", jmt_gemm(nullptr, nullptr));
   size_t ws = 0;
   for (int m = 1; m <= 1 << 16; m *= 7)

@@ -66,6 +66,11 @@ struct GemmParams {
   int c_vec8;                   // C rows / base 16-B aligned (16-bit C: paired 16-B stores)
   int dbg;                      // development ablations: 1 skip MFMA, 2 skip epilogue, 8 trace,
                                 //   16 split-K work dealt per (batch, split) as without splits
+  // row sums of A (the bias gradient of a weight-gradient GEMM dW = dY^T X: db = sum_k A[m][k]):
+  // dbias_tab[b0][m] (+)= ..., per-split fp32 partials in dbias_ws when split
+  float* dbias_tab[MAXP];
+  float* dbias_ws;
+  int n_dbias, dbias_acc;
 };
 
 // PF: A-fragment prefetch distance in MFMA rows; PRIO: s_setprio(1) around each MFMA row;
@@ -384,6 +389,60 @@ __device__ __forceinline__ void sgb_ds_reads(int n) {   // sched_group_barrier n
 struct NoIssue {
   __device__ __forceinline__ void operator()(int) const {}
 };
+
+// Row sums of the A operand (launches with n_dbias > 0: the bias gradient db = sum_k dY^T[m][k]
+// of a weight-gradient GEMM, taken from the A image already in LDS instead of a second pass over
+// dY in HBM).  M-subtile i of a block's row panel is summed by wave wn = i % WN of the n-tile
+// (i / WN) % tiles_n — spread over the waves and n-tiles, so a wave re-reads at most
+// ceil(TM / WN) fragments per k-step (for the 256x256 tile of an N = 512 wgrad: one).  After
+// the MFMAs of a K-tile (before the barrier that frees its stage) the owner reads the fragment
+// again and adds its 8 k-values with four v_dot2 against the literal (1, 1): one fp32 per lane,
+// the four k-groups folded at the end.  (Folded into the MFMA loop instead — as an MFMA against
+// an all-ones fragment, or as dot2s on the fragments in flight — the extra registers or the
+// owner branch inside the unrolled block spilled the 256x256 and 4-block tiles: +14-44 % on the
+// qkv / cross-attention wgrads, profiles/r03_wgrad_dbias.jsonl.)
+struct NoRowSums {
+  static constexpr bool on = false;
+};
+template <class C> struct RowSums {
+  static constexpr bool on = true;
+  static constexpr int NV = (C::TM + C::WN - 1) / C::WN;
+  float v[NV];
+  uint32_t own;     // bit i: this wave sums m-subtile i (wave-uniform)
+};
+
+__device__ __forceinline__ float rowsum8(bf16x8 a, float c) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 one = {(__bf16)1.0f, (__bf16)1.0f};
+  c = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(a, a, 0, 1), one, c, false);
+  c = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(a, a, 2, 3), one, c, false);
+  c = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(a, a, 4, 5), one, c, false);
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(a, a, 6, 7), one, c, false);
+}
+__device__ __forceinline__ float rowsum8(f16x8 a, float c) {
+  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+  const f16x2 one = {(_Float16)1.0f, (_Float16)1.0f};
+  c = __builtin_amdgcn_fdot2(__builtin_shufflevector(a, a, 0, 1), one, c, false);
+  c = __builtin_amdgcn_fdot2(__builtin_shufflevector(a, a, 2, 3), one, c, false);
+  c = __builtin_amdgcn_fdot2(__builtin_shufflevector(a, a, 4, 5), one, c, false);
+  return __builtin_amdgcn_fdot2(__builtin_shufflevector(a, a, 6, 7), one, c, false);
+}
+template <bool RS, class C> struct RowSumSel { typedef NoRowSums type; };
+template <class C> struct RowSumSel<true, C> { typedef RowSums<C> type; };
+
+template <typename T, bool AK, class C>
+__device__ __forceinline__ void rowsum_tile(const char* imgA, int wm, int wn, RowSums<C>& rs) {
+  constexpr int KS = C::KB / 64;
+#pragma unroll
+  for (int sl = 0; sl < RowSums<C>::NV; ++sl) {
+    const int i = sl * C::WN + wn;
+    if (i >= C::TM || !((rs.own >> i) & 1u)) continue;     // wave-uniform
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      rs.v[sl] = rowsum8(read_frag16<T, AK, C::KB, C::BM>(imgA, wm * C::WTM + i * 16, ks),
+                         rs.v[sl]);
+  }
+}
 
 template <typename T, bool AK, bool BK, class C, class ISSUE = NoIssue>
 __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB, int wm, int wn,
@@ -770,7 +829,29 @@ __device__ __forceinline__ void trace_stamp(const GemmParams& p, int slot) {
 // One block per output tile (blockIdx.x, XCD-remapped), batch entry (blockIdx.y) and K split
 // (blockIdx.z).  (A persistent form — blocks capped at the resident slots, the next tile's first
 // K-tile prefetched under the epilogue — measured 3-5% slower: profiles/r01_gemm_persistent.txt.)
-template <typename T, typename O, bool AK, bool BK, class C>
+// A row sums of one block (RowSums above) -> dbias_tab[b0][m] (+)=, or the split's fp32 partial
+template <class C>
+__device__ __forceinline__ void rowsum_store(const GemmParams& p, const GemmWork& wk,
+                                             const RowSums<C>& rs, int lane, int wm) {
+  const int nb = p.batch0 * p.batch1;
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i) {
+    if (!((rs.own >> i) & 1u)) continue;                  // wave-uniform
+    float v = rs.v[i / C::WN];
+    v += __shfl_xor(v, 16);                                // the four k-groups of row lane & 15
+    v += __shfl_xor(v, 32);
+    const int m = wk.m0 + wm * C::WTM + 16 * i + lane;
+    if (lane >= 16 || m >= p.M) continue;
+    if (p.splits > 1) {
+      p.dbias_ws[((int64_t)wk.split * nb + wk.b) * p.M + m] = v;
+    } else {
+      float* d = p.dbias_tab[wk.b0];
+      d[m] = (p.dbias_acc ? d[m] : 0.f) + v;
+    }
+  }
+}
+
+template <typename T, typename O, bool AK, bool BK, class C, bool RS = false>
 __global__ __launch_bounds__(C::NT, C::OCC)
 void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -798,6 +879,19 @@ void gemm_kernel(GemmParams p) {
   for (int i = 0; i < C::TM; ++i)
 #pragma unroll
     for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  typedef typename RowSumSel<RS, C>::type RSumT;
+  RSumT rsum;
+  [[maybe_unused]] const int wnu = __builtin_amdgcn_readfirstlane(wn);
+  if constexpr (RS) {
+    const int tn = cur.n0 / C::BN;
+    uint32_t own = 0;
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+      if (i % C::WN == wnu && (i / C::WN) % p.tiles_n == tn) own |= 1u << i;
+    rsum.own = own;
+#pragma unroll
+    for (int v = 0; v < RSumT::NV; ++v) rsum.v[v] = 0.f;
+  }
 
   if constexpr (C::S == 2) {
     // prefetch one tile, two barriers per tile
@@ -815,6 +909,7 @@ void gemm_kernel(GemmParams p) {
       if (kt == 0) trace_stamp(p, 1);
       const char* img = smem + (kt & 1) * C::STAGE;
       if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
+      if constexpr (RS) rowsum_tile<T, AK, C>(img, wm, wnu, rsum);
       __builtin_amdgcn_s_barrier();            // buffer (kt&1) free for tile kt+2
     }
   } else if constexpr (C::IL) {
@@ -872,6 +967,7 @@ void gemm_kernel(GemmParams p) {
       const char* img = smem + (kt % C::S) * C::STAGE;
       if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc, issue);
       else issue(0);
+      if constexpr (RS) rowsum_tile<T, AK, C>(img, wm, wnu, rsum);
     }
   } else {
     // S-1 tiles in flight, one barrier per tile: the barrier of iteration kt also certifies that
@@ -889,6 +985,7 @@ void gemm_kernel(GemmParams p) {
         issue_ktile<T, AK, BK, C>(p, smem, cur, kt + C::S - 1, (kt + C::S - 1) % C::S);
       const char* img = smem + (kt % C::S) * C::STAGE;
       if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
+      if constexpr (RS) rowsum_tile<T, AK, C>(img, wm, wnu, rsum);
     }
   }
   if (tail) {   // trailing partial K-tile: masked register staging
@@ -905,10 +1002,12 @@ void gemm_kernel(GemmParams p) {
     stage_tile<T, BK, C::KB, C::BN, C::NT>(base + IA, B, p.ldb, p.N, cur.n0, kb_lim, kb);
     __syncthreads();
     if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(base, base + IA, wm, wn, acc);
+    if constexpr (RS) rowsum_tile<T, AK, C>(base, wm, wnu, rsum);
   }
   __syncthreads();
   trace_stamp(p, 2);
   gemm_epilogue<T, O, C>(p, cur, acc, lane, wm, wn);
+  if constexpr (RS) rowsum_store<C>(p, cur, rsum, lane, wm);
   trace_stamp(p, 3);
 }
 
@@ -955,6 +1054,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
       }
     }
     const int b0 = b / p.batch1, b1 = b % p.batch1;
+    if (p.n_dbias > 0 && n == 0) {   // the A row sums' split partials, in split order
+      const float* src = p.dbias_ws + (int64_t)b * p.M + m;
+      float r = 0.f;
+      for (int t = 0; t < p.splits; ++t) r += src[(int64_t)t * nb * p.M];
+      float* d = p.dbias_tab[b0];
+      d[m] = (p.dbias_acc ? d[m] : 0.f) + r;
+    }
     const float* biasp = p.n_bias > 0 ? p.bias_tab[b0] : p.bias;
     O* cp;
     int64_t cbase;
@@ -996,9 +1102,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
 }
 
 // ------------------------------------------------------------------ launch
-template <typename T, typename O, bool AK, bool BK, class C>
+template <typename T, typename O, bool AK, bool BK, class C, bool RS = false>
 static void launch_cfg(const GemmParams& p, dim3 grid, hipStream_t st) {
-  auto fn = gemm_kernel<T, O, AK, BK, C>;
+  auto fn = gemm_kernel<T, O, AK, BK, C, RS>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1008,21 +1114,21 @@ static void launch_cfg(const GemmParams& p, dim3 grid, hipStream_t st) {
   hipLaunchKernelGGL(fn, grid, dim3(C::NT), (size_t)C::LDS, st, p);
 }
 
-template <typename T, typename O, bool AK, bool BK>
+template <typename T, typename O, bool AK, bool BK, bool RS = false>
 static void launch_layout(const GemmParams& p, int cfg, dim3 grid, hipStream_t st) {
   switch (cfg) {
-    case 5: launch_cfg<T, O, AK, BK, Cfg5>(p, grid, st); break;
-    case 30: if constexpr (AK) { launch_cfg<T, O, AK, BK, Cfg30>(p, grid, st); break; }
+    case 5: launch_cfg<T, O, AK, BK, Cfg5, RS>(p, grid, st); break;
+    case 30: if constexpr (AK) { launch_cfg<T, O, AK, BK, Cfg30, RS>(p, grid, st); break; }
              [[fallthrough]];
-    case 10: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg10>(p, grid, st); break; }
+    case 10: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg10, RS>(p, grid, st); break; }
              [[fallthrough]];
-    case 11: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg11>(p, grid, st); break; }
+    case 11: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg11, RS>(p, grid, st); break; }
              [[fallthrough]];
-    case 20: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg20>(p, grid, st); break; }
+    case 20: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg20, RS>(p, grid, st); break; }
              [[fallthrough]];
-    case 21: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg21>(p, grid, st); break; }
+    case 21: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg21, RS>(p, grid, st); break; }
              [[fallthrough]];
-    default: launch_cfg<T, O, AK, BK, Cfg1>(p, grid, st); break;
+    default: launch_cfg<T, O, AK, BK, Cfg1, RS>(p, grid, st); break;
   }
 }
 
@@ -1031,7 +1137,13 @@ static void launch_to(const GemmParams& p, int ak, int bk, int cfg, dim3 grid, h
   if (ak && bk) launch_layout<T, O, true, true>(p, cfg, grid, st);
   else if (ak && !bk) launch_layout<T, O, true, false>(p, cfg, grid, st);
   else if (!ak && bk) launch_layout<T, O, false, true>(p, cfg, grid, st);
-  else launch_layout<T, O, false, false>(p, cfg, grid, st);
+  else if constexpr (sizeof(T) == 2 && sizeof(O) == 4) {
+    // weight gradients (fp32 out): A row sums only on this layout (jmt_gemm checks)
+    if (p.n_dbias > 0) launch_layout<T, O, false, false, true>(p, cfg, grid, st);
+    else launch_layout<T, O, false, false>(p, cfg, grid, st);
+  } else {
+    launch_layout<T, O, false, false>(p, cfg, grid, st);
+  }
 }
 
 template <typename T>
@@ -1225,6 +1337,19 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   p.c_dtype = d->c_dtype;
   p.aux_dtype = d->aux_dtype;
   p.dbg = g_gemm_dbg;
+  JMT_CHECK_ARG(d->n_dbias >= 0 && d->n_dbias <= MAXP, "jmt_gemm: dbias table size");
+  p.n_dbias = d->n_dbias;
+  p.dbias_acc = d->dbias_acc;
+  p.dbias_ws = d->dbias_ws;
+  for (int i = 0; i < MAXP; ++i) p.dbias_tab[i] = i < d->n_dbias ? d->dbias_tab[i] : nullptr;
+  if (d->n_dbias > 0) {
+    JMT_CHECK_ARG(dt != JMT_F32 && d->c_dtype == JMT_F32 && !d->a_kmajor && !d->b_kmajor &&
+                      batch1 == 1 && d->n_dbias >= batch0,
+                  "jmt_gemm: A row sums need 16-bit MN-major A and B, fp32 C, batch1 = 1 and a "
+                  "dbias table of batch0 entries");
+    for (int i = 0; i < batch0; ++i)
+      JMT_CHECK_ARG(d->dbias_tab[i] != nullptr, "jmt_gemm: null dbias_tab[%d]", i);
+  }
   {
     const int ces = dtype_size(d->c_dtype);
     bool cv4 = d->ldc % 4 == 0 && d->sC0 % 4 == 0 && d->sC1 % 4 == 0;
@@ -1249,6 +1374,11 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
     const size_t need = jmt_gemm_workspace_bytes(d->M, d->N, batch0 * batch1, splits);
     JMT_CHECK_ARG(d->workspace != nullptr && d->ws_bytes >= need,
                   "jmt_gemm: split-K needs %zu workspace bytes", need);
+    if (d->n_dbias > 0) {
+      const size_t dneed = (size_t)splits * batch0 * (size_t)d->M * sizeof(float);
+      JMT_CHECK_ARG(d->dbias_ws != nullptr && d->dbias_ws_bytes >= dneed,
+                    "jmt_gemm: split-K A row sums need %zu dbias_ws bytes", dneed);
+    }
   }
   int cfg = g_gemm_cfg;
   if (dt == JMT_F32 && cfg >= 10) cfg = 1;   // occupancy configs: 16-bit only
@@ -1263,6 +1393,10 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
       if (t) cfg = t;
     }
   }
+  // A row sums: the 4-block 128x128 tile (128 VGPRs) spills with the extra per-lane sums; the
+  // 256x256 tile does not and runs the split-K qkv / FFN wgrad shapes at least as fast
+  // (profiles/r03_wgrad_dbias.jsonl)
+  if (d->n_dbias > 0 && cfg == 10) cfg = 5;
   int bm, bn;
   cfg_tile(cfg, bm, bn);
   p.tiles_m = (d->M + bm - 1) / bm;

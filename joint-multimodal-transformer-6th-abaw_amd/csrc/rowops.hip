@@ -113,7 +113,13 @@ __global__ __launch_bounds__(RB) void ln_fwd_kernel(int64_t rows, int D, const T
   }
 }
 
-constexpr int LN_ROWS_PER_BLOCK = 16;    // 4 rows per wave (1200 blocks at B*T = 19200)
+// LayerNorm backward rows per block (partials: ceil(rows / 16) blocks).  Each block writes NS*D
+// fp32 partials, so the grouped launch (G x more blocks) takes 32 rows per block: half the
+// partial traffic (37 % of the row bytes at D = 512) — 57.6 -> 54.4 us at G = 3, 129.5 ->
+// 123.4 at G = 6; one group alone keeps 16 (1200 blocks; 32 measured 69 -> 80 us for three
+// separate launches): profiles/r03_rowops.jsonl, r03_rowops_ln32.jsonl
+constexpr int LN_ROWS_PER_BLOCK = 16;
+constexpr int LN_ROWS_PER_BLOCK_GROUPED = 32;
 
 // 4-element vector loads/stores (8 B for 16-bit types, 16 B for f32); rows are 4-aligned
 template <typename T> struct V4;
@@ -252,7 +258,8 @@ __global__ __launch_bounds__(RB) void ln_fwd_vec_kernel(int64_t rows, const TI* 
 }
 
 // NV = D / 256: lane owns elements 4*(lane + 64 j) .. +3, j < NV
-template <typename TI, typename TG, typename TD, int NV, bool DS = false>
+template <typename TI, typename TG, typename TD, int NV, bool DS = false,
+          int RPB = LN_ROWS_PER_BLOCK>
 __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* x, int64_t ldx,
                                                         const TI* rr, int64_t ldr, const TG* dy,
                                                         int64_t lddy, const float* mean,
@@ -283,46 +290,64 @@ __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* 
 #pragma unroll
     for (int e = 0; e < 4; ++e) pg[j][e] = pb[j][e] = ps[j][e] = 0.f;
   }
-  const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK;
-  for (int i = w; i < LN_ROWS_PER_BLOCK; i += 4) {
-    const int64_t r = rbeg + i;
-    if (r >= rows) break;
-    const float mu = mean[r], rs = rstd[r];
-    float xh[NV][4], gd[NV][4];
-    float s1 = 0.f, s2 = 0.f;
+  const int64_t rbeg = (int64_t)blockIdx.x * RPB;
+  // two rows per wave per iteration, both rows' loads issued before either is reduced (rows past
+  // the end are clamped for the loads and skipped for the math: wave-uniform)
+  for (int i0 = w; i0 < RPB; i0 += 8) {
+    float xv[2][NV][4], gv[2][NV][4], mu[2], rs[2];
+    int64_t rw[2];
+    bool ok[2];
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int c = 4 * (lane + 64 * j);
-      float xv[4], gv[4];
-      V4<TI>::ld(x + r * ldx + c, xv);
-      if (rr) {
-        float rv[4];
-        V4<TI>::ld(rr + r * ldr + c, rv);
+    for (int u = 0; u < 2; ++u) {
+      const int64_t r = rbeg + i0 + 4 * u;
+      ok[u] = r < rows;
+      const int64_t rc = ok[u] ? r : rows - 1;
+      rw[u] = rc;
+      mu[u] = mean[rc];
+      rs[u] = rstd[rc];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) xv[e] += rv[e];
-      }
-      V4<TG>::ld(dy + r * lddy + c, gv);
+      for (int j = 0; j < NV; ++j) {
+        const int c = 4 * (lane + 64 * j);
+        V4<TI>::ld(x + rc * ldx + c, xv[u][j]);
+        if (rr) {
+          float rv[4];
+          V4<TI>::ld(rr + rc * ldr + c, rv);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        xh[j][e] = (xv[e] - mu) * rs;
-        pg[j][e] += gv[e] * xh[j][e];
-        pb[j][e] += gv[e];
-        gd[j][e] = gv[e] * gm[j][e];
-        s1 += gd[j][e];
-        s2 += gd[j][e] * xh[j][e];
+          for (int e = 0; e < 4; ++e) xv[u][j][e] += rv[e];
+        }
+        V4<TG>::ld(dy + rc * lddy + c, gv[u][j]);
       }
     }
-    s1 = wave_sum(s1) * (1.f / D);
-    s2 = wave_sum(s2) * (1.f / D);
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      float o[4];
+    for (int u = 0; u < 2; ++u) {
+      if (!ok[u]) continue;
+      const int64_t r = rw[u];
+      float xh[NV][4], gd[NV][4];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = rs * (gd[j][e] - s1 - xh[j][e] * s2);
-      V4<TD>::st(dx + r * lddx + 4 * (lane + 64 * j), o);
-      if constexpr (DS) {
+      for (int j = 0; j < NV; ++j) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ps[j][e] += o[e];
+        for (int e = 0; e < 4; ++e) {
+          xh[j][e] = (xv[u][j][e] - mu[u]) * rs[u];
+          pg[j][e] += gv[u][j][e] * xh[j][e];
+          pb[j][e] += gv[u][j][e];
+          gd[j][e] = gv[u][j][e] * gm[j][e];
+          s1 += gd[j][e];
+          s2 += gd[j][e] * xh[j][e];
+        }
+      }
+      s1 = wave_sum(s1) * (1.f / D);
+      s2 = wave_sum(s2) * (1.f / D);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rs[u] * (gd[j][e] - s1 - xh[j][e] * s2);
+        V4<TD>::st(dx + r * lddx + 4 * (lane + 64 * j), o);
+        if constexpr (DS) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ps[j][e] += o[e];
+        }
       }
     }
   }
@@ -1043,10 +1068,11 @@ extern "C" int jmt_layernorm_bwd_grouped(int dt_in, int dt_dy, int dt_dx, int G,
     t2.p[g] = dsum ? dsum[g] : nullptr;
   }
   hipStream_t st = as_stream(stream);
-  const int nblk = jmt_layernorm_bwd_blocks(rows);
+  const int nblk = (int)((rows + LN_ROWS_PER_BLOCK_GROUPED - 1) / LN_ROWS_PER_BLOCK_GROUPED);
   const dim3 grid((unsigned)nblk, (unsigned)G);
 #define JMT_LNBG(NV, DS)                                                                         \
-  hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV, DS>), grid, dim3(RB), 0, st, rows,     \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV, DS, LN_ROWS_PER_BLOCK_GROUPED>), grid,  \
+                     dim3(RB), 0, st, rows,                                                     \
                      (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd,     \
                      grp.gamma[0], (TD*)dx, lddx, partials, grp)
   JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_dy, TG, JMT_DISPATCH1(dt_dx, TD,

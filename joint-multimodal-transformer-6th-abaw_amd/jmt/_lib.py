@@ -42,6 +42,8 @@ class GemmDesc(C.Structure):
         ("splits", c_int),
         ("workspace", c_vp), ("ws_bytes", C.c_size_t),
         ("bias_tab", c_vp * 8), ("n_bias", c_int),
+        ("dbias_tab", c_vp * 8), ("n_dbias", c_int), ("dbias_acc", c_int),
+        ("dbias_ws", c_vp), ("dbias_ws_bytes", C.c_size_t),
     ]
 
 
@@ -163,7 +165,7 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.jmt_abi_version() != 3:
+    if lib.jmt_abi_version() != 4:
         raise JMTError("libjmt_hip.so ABI version mismatch")
     cfg = int(os.environ.get("JMT_GEMM_CFG", "0"))   # development: force a GEMM pipeline config
     dbg = int(os.environ.get("JMT_GEMM_DBG", "0"))   # development: gemm.hip ablation flags

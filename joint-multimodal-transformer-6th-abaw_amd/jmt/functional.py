@@ -250,13 +250,29 @@ def _dgrad(G: Rows, n, W, r0, cd, outs, ld_out, nseg, kseg, aux=None, ldaux=0, b
              aux=aux, ldaux=ldaux, device=G.t.device)
 
 
-def _wgrad(G: Rows, n, xin, ld_in, kseg, W, r0, cd):
-    """W.grad[r0:r0+n, s*kseg:...] += dY^T X_s   (split-K over the rows)."""
+_fused_bgrad = {"on": os.environ.get("JMT_FUSED_BGRAD", "1") != "0"}
+
+
+def fused_bgrad_ok(cd) -> bool:
+    """Bias gradients as the A row sums of their weight-gradient GEMM (jmt_gemm_desc.dbias_tab,
+    16-bit operands only); JMT_FUSED_BGRAD=0 keeps the separate column-sum launches."""
+    return _fused_bgrad["on"] and cd in (torch.bfloat16, torch.float16)
+
+
+def _wgrad(G: Rows, n, xin, ld_in, kseg, W, r0, cd, b=None) -> bool:
+    """W.grad[r0:r0+n, s*kseg:...] += dY^T X_s   (split-K over the rows); with `b`, also
+    b.grad[r0:r0+n] += the column sums of dY inside the same GEMM when the launch form allows it
+    (one K segment, n > 1, 16-bit).  Returns True when b.grad was written."""
     gW = _grad_buffer(W)
     if gW is None:
-        return
+        return False
     nseg = len(xin)
     Kin = W.shape[1]
+    dbt = None
+    if b is not None and n > 1 and nseg == 1 and fused_bgrad_ok(cd):
+        gb = _grad_buffer(b)
+        if gb is not None:
+            dbt = [gb[r0:r0 + n]]
     # A = dY^T (MN-major); for n == 1 the single row is the contiguous dY column (K-major)
     a_ld, a_kmaj = (G.ld, False) if n > 1 else (_vec(cd), True)
     ops.gemm(M=n, N=kseg, K=G.rows, ab_dtype=_dc(cd), c_dtype=F32,
@@ -264,8 +280,11 @@ def _wgrad(G: Rows, n, xin, ld_in, kseg, W, r0, cd):
              b=[x.data_ptr() for x in xin], ldb=ld_in, b_kmajor=False,
              b_mode=1 if nseg > 1 else 0,
              c=[_ptr(gW, r0 * Kin)], ldc=Kin, batch0=nseg, sA=(0, 0), sB=(0, 0),
-             sC=(kseg, 0), beta=1.0, device=G.t.device)
+             sC=(kseg, 0), beta=1.0, dbias_tab=dbt, device=G.t.device)
     _grad_done(W)
+    if dbt is not None:
+        _grad_done(b)
+    return dbt is not None
 
 
 def _bgrad(G: Rows, n, b, r0):
@@ -321,8 +340,8 @@ class LinearFn(Function):
                                                                                   in_dtypes[i])
 
         def param_grads():      # side stream (jmt.streams.run_side)
-            _wgrad(Gy, n, xin, L0.ld, kseg, W, r0, cd)
-            _bgrad(Gy, n, b, r0)
+            if not _wgrad(Gy, n, xin, L0.ld, kseg, W, r0, cd, b):
+                _bgrad(Gy, n, b, r0)
 
         streams.run_side(param_grads, reads=(Gy.t,) + tuple(xin))
         return (None, None, None, None, None, *dxs)
@@ -396,8 +415,8 @@ class MLPFn(Function):
                 dx = _cast_keep_layout(dx, xdt)
 
         def w1_grads():
-            _wgrad(Gh, hid, [xin], L.ld, L.F, W1, 0, cd)
-            _bgrad(Gh, hid, b1, 0)
+            if not _wgrad(Gh, hid, [xin], L.ld, L.F, W1, 0, cd, b1):
+                _bgrad(Gh, hid, b1, 0)
 
         streams.run_side(w1_grads, reads=(dh, xin))
         return None, None, None, None, None, dx

@@ -83,14 +83,24 @@ def _gemm_dgrad(dy_ptr: int, ldy: int, sdy: int, rows: int, n: int, Ws, r0: int,
 
 
 def _gemm_wgrad(dy_ptrs: Sequence[int], ldy: int, sdy: int, x_ptrs: Sequence[int], ldx: int,
-                sx: int, rows: int, n: int, Ws, r0: int, cd, dev):
+                sx: int, rows: int, n: int, Ws, r0: int, cd, dev, bs=None) -> bool:
     """W_g.grad[r0:r0+n] += dY[g]^T X[g]  (fp32, split-K over the rows).  dY / X are strided
     ([base], stride) or per-group pointer tables.  The Ws of one launch must be distinct
-    parameters (their gradient regions are written concurrently)."""
+    parameters (their gradient regions are written concurrently).  With `bs` (distinct bias
+    parameters), also b_g.grad[r0:r0+n] += the column sums of dY[g], taken inside the same GEMM
+    (functional.fused_bgrad_ok); returns True when the bias gradients were written."""
+    from .functional import fused_bgrad_ok
     grads = []
     for W in Ws:
         g = _grad_buffer(W)
         grads.append(g if g is not None else torch.zeros_like(W))
+    dbt = None
+    if bs is not None and n > 1 and fused_bgrad_ok(cd):
+        dbt = []
+        for b in bs:
+            gb = _grad_buffer(b)
+            dbt.append(gb[r0:r0 + n] if gb is not None else
+                       torch.empty(n, dtype=torch.float32, device=dev))
     Kin = Ws[0].shape[1]
     ta, tb = len(dy_ptrs) > 1, len(x_ptrs) > 1
     ops.gemm(M=n, N=Kin, K=rows, ab_dtype=_dc(cd), c_dtype=ops.F32,
@@ -99,8 +109,11 @@ def _gemm_wgrad(dy_ptrs: Sequence[int], ldy: int, sdy: int, x_ptrs: Sequence[int
              b=list(x_ptrs), ldb=ldx, b_kmajor=False, b_mode=1 if tb else 0,
              sB=(0 if tb else sx, 0),
              c=[_ptr(g, r0 * Kin) for g in grads], ldc=Kin, c_mode=1, batch0=len(Ws),
-             beta=1.0, device=dev)
+             beta=1.0, dbias_tab=dbt, device=dev)
     _grad_done(*Ws)
+    if dbt is not None:
+        _grad_done(*bs)
+    return dbt is not None
 
 
 def _bias_grad(dy2: torch.Tensor, ld: int, rows: int, n: int, b, r0: int):
@@ -279,8 +292,8 @@ class LastQueryMHAFn(Function):
         G = _match(gy.unsqueeze(0), Rows(O.like(E, cd)), cd)          # (1, N, E) in o's order
         do = O.like(E, cd)
         _dgrad(G, E, Wout, 0, cd, [do], _ld(do, O.perm), 1, E)
-        _wgrad(G, E, [O.t], O.ld, E, Wout, 0, cd)
-        _bgrad(G, E, bout, 0)
+        if not _wgrad(G, E, [O.t], O.ld, E, Wout, 0, cd, bout):
+            _bgrad(G, E, bout, 0)
         X = Rows(x)
         dkv = X.like(2 * E, cd)
         dq = Rows(q).like(E, cd)
@@ -288,14 +301,14 @@ class LastQueryMHAFn(Function):
         DKV = Rows(dkv)
         dx = X.like(E, cd)
         _dgrad(DKV, 2 * E, Win, E, cd, [dx], _ld(dx, X.perm), 1, E)
-        _wgrad(DKV, 2 * E, [X.t], X.ld, E, Win, E, cd)
-        _bgrad(DKV, 2 * E, bin_, E)
+        if not _wgrad(DKV, 2 * E, [X.t], X.ld, E, Win, E, cd, bin_):
+            _bgrad(DKV, 2 * E, bin_, E)
         DQ = Rows(dq)
         XL = Rows(x[-1:])
         dxl = dx[-1:]
         _dgrad(DQ, E, Win, 0, cd, [dxl], _ld(dxl, XL.perm), 1, E, beta=1.0)
-        _wgrad(DQ, E, [XL.t], XL.ld, E, Win, 0, cd)
-        _bgrad(DQ, E, bin_, 0)
+        if not _wgrad(DQ, E, [XL.t], XL.ld, E, Win, 0, cd, bin_):
+            _bgrad(DQ, E, bin_, 0)
         if xdt != cd:
             dx = _cast_keep_layout(dx, xdt)
         ctx.asaved = None
@@ -451,8 +464,9 @@ class EncoderGroupFn(Function):
                     R * hid, cdt, cd, dev, aux=F1, ldaux=hid)
         # (W2's weight gradient stays on the compute stream: on the side stream the in-place
         # dH1 below would have to wait for it, which measured slower, profiles/r02_side_stream.txt)
-        _gemm_wgrad([dS.data_ptr()], E, R * E, [F1.data_ptr()], hid, R * hid, R, E,
-                    [p[6] for p in P], 0, cd, dev)
+        b2_done = _gemm_wgrad([dS.data_ptr()], E, R * E, [F1.data_ptr()], hid, R * hid, R, E,
+                              [p[6] for p in P], 0, cd, dev,
+                              bs=None if b2_done else [p[7] for p in P]) or b2_done
         if not b2_done:
             _bias_grad_grouped(dS.data_ptr(), G, E, R * E, R, E, [p[7] for p in P], 0, cd, dev)
         # dH1 = dS2 + dF1 . W1  (in place on dS: beta = 1)
@@ -460,10 +474,10 @@ class EncoderGroupFn(Function):
                     E, R * E, cdt, cd, dev, beta=1.0)
 
         def w1_grads():         # side stream: dF1 and H1 are not written again
-            _gemm_wgrad([dF1.data_ptr()], hid, R * hid, [H1.data_ptr()], E, R * E, R, hid,
-                        [p[4] for p in P], 0, cd, dev)
-            _bias_grad_grouped(dF1.data_ptr(), G, hid, R * hid, R, hid, [p[5] for p in P], 0,
-                               cd, dev)
+            if not _gemm_wgrad([dF1.data_ptr()], hid, R * hid, [H1.data_ptr()], E, R * E, R,
+                               hid, [p[4] for p in P], 0, cd, dev, bs=[p[5] for p in P]):
+                _bias_grad_grouped(dF1.data_ptr(), G, hid, R * hid, R, hid, [p[5] for p in P], 0,
+                                   cd, dev)
 
         streams.run_side(w1_grads, reads=(dF1, H1))
         # LN1: dS1 = d(X + A1)
@@ -476,9 +490,10 @@ class EncoderGroupFn(Function):
                     R * E, cdt, cd, dev)
 
         def out_proj_grads():   # side stream, under the attention backward
-            _gemm_wgrad([dS1.data_ptr()], E, R * E, o_ptrs, E, R * E if len(o_ptrs) == 1 else 0,
-                        R, E, [p[2] for p in P], 0, cd, dev)
-            if not bo_done:
+            done = _gemm_wgrad([dS1.data_ptr()], E, R * E, o_ptrs, E,
+                               R * E if len(o_ptrs) == 1 else 0, R, E, [p[2] for p in P], 0, cd,
+                               dev, bs=None if bo_done else [p[3] for p in P])
+            if not (bo_done or done):
                 _bias_grad_grouped(dS1.data_ptr(), G, E, R * E, R, E, [p[3] for p in P], 0, cd,
                                    dev)
 
@@ -497,10 +512,10 @@ class EncoderGroupFn(Function):
                     dS1.data_ptr(), E, R * E, cdt, cd, dev, beta=1.0)
 
         def in_proj_grads():    # side stream: dQKV and X are not written again
-            _gemm_wgrad([dQKV.data_ptr()], 3 * E, R * 3 * E, [X.data_ptr()], E, R * E, R, 3 * E,
-                        [p[0] for p in P], 0, cd, dev)
-            _bias_grad_grouped(dQKV.data_ptr(), G, 3 * E, R * 3 * E, R, 3 * E,
-                               [p[1] for p in P], 0, cd, dev)
+            if not _gemm_wgrad([dQKV.data_ptr()], 3 * E, R * 3 * E, [X.data_ptr()], E, R * E, R,
+                               3 * E, [p[0] for p in P], 0, cd, dev, bs=[p[1] for p in P]):
+                _bias_grad_grouped(dQKV.data_ptr(), G, 3 * E, R * 3 * E, R, 3 * E,
+                                   [p[1] for p in P], 0, cd, dev)
 
         streams.run_side(in_proj_grads, reads=(dQKV, X))
         ctx.state = None
@@ -587,11 +602,14 @@ class CrossAttention6Fn(Function):
                     dO.data_ptr(), E, R * E, cdt, cd, dev)
 
         def out_proj_grads():
+            rest = []
             for h in halves:
-                _gemm_wgrad([_ptr(dO6, i * R * E) for i in h], E, 0,
-                            [O[i * B].data_ptr() for i in h], E, 0, R, E,
-                            [M[pairs[i][0]][2] for i in h], 0, cd, dev)
-            for h in halves:
+                if not _gemm_wgrad([_ptr(dO6, i * R * E) for i in h], E, 0,
+                                   [O[i * B].data_ptr() for i in h], E, 0, R, E,
+                                   [M[pairs[i][0]][2] for i in h], 0, cd, dev,
+                                   bs=[M[pairs[i][0]][3] for i in h]):
+                    rest.append(h)
+            for h in rest:
                 if _consecutive(h):
                     _bias_grad_grouped(_ptr(dO6, h[0] * R * E), len(h), E, R * E, R, E,
                                        [M[pairs[i][0]][3] for i in h], 0, cd, dev)
@@ -608,14 +626,20 @@ class CrossAttention6Fn(Function):
         # in_proj weight gradients (side stream, overlapping the stream dgrads): query rows
         # [0, E) from the query stream, key/value rows [E, 3E) from the key stream
         def in_proj_grads():
+            rest = []
             for h in halves:
                 ws = [M[pairs[i][0]][0] for i in h]
-                _gemm_wgrad([_ptr(dQKV, i * R * 3 * E) for i in h], 3 * E, 0,
-                            [Y[pairs[i][1]].data_ptr() for i in h], E, 0, R, E, ws, 0, cd, dev)
-                _gemm_wgrad([_ptr(dQKV, i * R * 3 * E + E) for i in h], 3 * E, 0,
-                            [Y[pairs[i][2]].data_ptr() for i in h], E, 0, R, 2 * E, ws, E, cd,
-                            dev)
-            for h in halves:
+                bs = [M[pairs[i][0]][1] for i in h]
+                fq = _gemm_wgrad([_ptr(dQKV, i * R * 3 * E) for i in h], 3 * E, 0,
+                                 [Y[pairs[i][1]].data_ptr() for i in h], E, 0, R, E, ws, 0, cd,
+                                 dev, bs=bs)
+                fkv = _gemm_wgrad([_ptr(dQKV, i * R * 3 * E + E) for i in h], 3 * E, 0,
+                                  [Y[pairs[i][2]].data_ptr() for i in h], E, 0, R, 2 * E, ws, E,
+                                  cd, dev, bs=bs if fq else None)
+                if not (fq and fkv):
+                    assert not fq, "query-row bias sums fused without the key / value rows"
+                    rest.append(h)
+            for h in rest:
                 if _consecutive(h):
                     _bias_grad_grouped(_ptr(dQKV, h[0] * R * 3 * E), len(h), 3 * E, R * 3 * E,
                                        R, 3 * E, [M[pairs[i][0]][1] for i in h], 0, cd, dev)

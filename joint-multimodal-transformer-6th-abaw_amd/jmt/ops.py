@@ -61,7 +61,10 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
          batch0: int = 1, batch1: int = 1, sA=(0, 0), sB=(0, 0), sC=(0, 0),
          alpha: float = 1.0, beta: float = 0.0, bias: Optional[torch.Tensor] = None,
          bias_mode: int = 1, relu: bool = False, aux: Optional[torch.Tensor] = None,
-         ldaux: int = 0, splits: Optional[int] = None, bias_tab=None, device=None) -> None:
+         ldaux: int = 0, splits: Optional[int] = None, bias_tab=None, dbias_tab=None,
+         dbias_acc: bool = True, device=None) -> None:
+    """dbias_tab: per-b0 fp32 outputs that receive (dbias_acc: += ) the row sums of A — a
+    weight-gradient GEMM's bias gradient (jmt_gemm_desc ABI 4)."""
     d = GemmDesc()
     d.ab_dtype, d.c_dtype = ab_dtype, c_dtype
     d.aux_dtype = dt(aux) if aux is not None else c_dtype
@@ -94,9 +97,21 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
         splits = auto_splits(M, N, K, batch0 * batch1, ab_dtype)
     d.splits = splits
     ws = None
+    if dbias_tab:
+        for i, t in enumerate(dbias_tab):
+            d.dbias_tab[i] = t.data_ptr()
+        d.n_dbias = len(dbias_tab)
+        d.dbias_acc = int(dbias_acc)
     if splits > 1:
         nbytes = _lib.load().jmt_gemm_workspace_bytes(M, N, batch0 * batch1, splits)
-        ws = workspace(nbytes, device)
+        if dbias_tab:
+            # the A row sums' split partials after the slabs (16-B aligned: the slab bytes are)
+            dbytes = splits * batch0 * M * 4
+            ws = workspace(nbytes + dbytes, device)
+            d.dbias_ws = ws.data_ptr() + nbytes
+            d.dbias_ws_bytes = dbytes
+        else:
+            ws = workspace(nbytes, device)
         d.workspace = ws.data_ptr()
         d.ws_bytes = nbytes
     launch = lambda: _lib.check(_lib.load().jmt_gemm(C.byref(d), stream()), "jmt_gemm")
@@ -106,6 +121,7 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
         _launch_hook({"family": fam, "ab_dtype": ab_dtype, "c_dtype": c_dtype,
                       "a_kmajor": bool(a_kmajor), "b_kmajor": bool(b_kmajor), "M": M, "N": N,
                       "K": K, "batch": batch0 * batch1, "beta": beta,
+                      "dbias": bool(dbias_tab),
                       "flops": 2.0 * M * N * K * batch0 * batch1,
                       "bytes": batch0 * batch1 * ((M + N) * K * (4 if ab_dtype == F32 else 2) +
                                                   M * N * (4 if c_dtype == F32 else 2)),

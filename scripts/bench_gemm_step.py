@@ -49,6 +49,12 @@ def make_shapes(R):
         ("ca wgrad b6 TN 1024x512xR", 1024, 512, R, False, False, 6, F32, {"beta": 1.0}),
         ("ca wgrad b6 TN 512x512xR", 512, 512, R, False, False, 6, F32, {"beta": 1.0}),
         ("enc wgrad b3 TN 512x1536xR", 512, 1536, R, False, False, 3, F32, {"beta": 1.0}),
+        # round 3: the same weight gradients with their bias gradients as A row sums (dbias_tab)
+        ("wgrad b3 TN 512x512xR +dbias", 512, 512, R, False, False, 3, F32, {"beta": 1.0, "dbias": True}),
+        ("wgrad b3 TN 1536x512xR +dbias", 1536, 512, R, False, False, 3, F32, {"beta": 1.0, "dbias": True}),
+        ("ca wgrad b6 TN 1024x512xR +dbias", 1024, 512, R, False, False, 6, F32, {"beta": 1.0, "dbias": True}),
+        ("ca wgrad b6 TN 512x512xR +dbias", 512, 512, R, False, False, 6, F32, {"beta": 1.0, "dbias": True}),
+        ("enc wgrad b3 TN 512x1536xR +dbias", 512, 1536, R, False, False, 3, F32, {"beta": 1.0, "dbias": True}),
         ("video linear fwd NT 512x2048", R, 512, 2048, True, True, 1, BF16, {}),
         ("fc fwd NT 512x1024", R, 512, 1024, True, True, 1, BF16, {}),
         ("pv dgrad NN 1024x512 b1", R, 1024, 512, True, False, 1, BF16, {}),
@@ -88,6 +94,8 @@ def run(reps, cfg, dbg=0, splits=None):
                 kw.update(b=[Bt[0][i].data_ptr() for i in range(batch)], b_mode=1)
             else:
                 kw.update(b=[Bt[0].data_ptr()], sB=(Bt[0].shape[1], 0))
+        if ex.get("dbias"):
+            kw.update(dbias_tab=[torch.zeros(M, device=dev) for _ in range(batch)])
         for _ in range(3):
             ws = ops.gemm(**kw)
         torch.cuda.synchronize()

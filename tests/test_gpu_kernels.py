@@ -861,3 +861,53 @@ def test_layernorm_grouped_equals_per_group(dsum, cd):
         assert torch.equal(a[1][i], b[1][i]) and torch.equal(a[2][i], b[2][i])
         if dsum:
             assert torch.equal(a[3][i], b[3][i])
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 5, 10, 11, 20, 21])
+@pytest.mark.parametrize("dt", [BF16, F16])
+def test_gemm_wgrad_row_sums_bias_grad(cfg, dt):
+    """jmt_gemm's A row sums (dbias_tab, ABI 4): a weight-gradient GEMM dW = dY^T X also writes
+    the bias gradient db = column sums of dY from the A fragments it already holds.  vs the fp32
+    column sums of the same rounded dY, with and without split-K, accumulate and overwrite,
+    ragged M / K, pointer-table batch; C is bit-identical to the same launch without row sums."""
+    from jmt import _lib
+    lib = _lib.load()
+    t = TD[dt]
+    g = torch.Generator(device=DEV).manual_seed(41)
+    lib.jmt_gemm_set_debug(cfg << 8)
+    try:
+        for (n, Kin, rows, batch, splits, acc) in [(300, 520, 1000, 2, 1, True),
+                                                   (512, 512, 19200, 3, None, True),
+                                                   (257, 129, 333, 1, 3, False),
+                                                   (1536, 512, 4800, 1, None, True),
+                                                   (40, 64, 4096, 2, 8, False)]:
+            ldn, ldk = _rup(n, 8) + 8, _rup(Kin, 8) + 8
+            dY = torch.randn(batch, rows, ldn, device=DEV, generator=g).to(t)
+            X = torch.randn(batch, rows, ldk, device=DEV, generator=g).to(t)
+            C0 = torch.randn(batch, n, Kin, device=DEV, generator=g)
+            C1 = C0.clone()
+            db = [torch.randn(n, device=DEV, generator=g) for _ in range(batch)]
+            db0 = [d.clone() for d in db]
+            kw = dict(M=n, N=Kin, K=rows, ab_dtype=dt, c_dtype=F32,
+                      a=[dY[i].data_ptr() for i in range(batch)], lda=ldn, a_kmajor=False,
+                      a_mode=1, b=[X[i].data_ptr() for i in range(batch)], ldb=ldk,
+                      b_kmajor=False, b_mode=1, ldc=Kin, c_mode=1, batch0=batch, beta=1.0,
+                      splits=splits, device=DEV)
+            ops.gemm(c=[C0[i].data_ptr() for i in range(batch)], **kw)
+            ops.gemm(c=[C1[i].data_ptr() for i in range(batch)], dbias_tab=db, dbias_acc=acc,
+                     **kw)
+            torch.cuda.synchronize()
+            assert torch.equal(C0, C1), (cfg, n, Kin, rows, "C changed by the row sums")
+            for i in range(batch):
+                ref = dY[i, :, :n].float().sum(0) + (db0[i] if acc else 0.0)
+                err = (db[i] - ref).abs().max().item()
+                scale = dY[i, :, :n].float().abs().sum(0).max().item()
+                assert err <= 1e-6 * scale + 1e-5, (cfg, n, Kin, rows, splits, i, err)
+        with pytest.raises(_lib.JMTError):    # K-major A: not a weight-gradient launch
+            A = torch.randn(64, 64, device=DEV).to(t)
+            C = torch.empty(64, 64, device=DEV)
+            ops.gemm(M=64, N=64, K=64, ab_dtype=dt, c_dtype=F32, a=[A.data_ptr()], lda=64,
+                     a_kmajor=True, b=[A.data_ptr()], ldb=64, b_kmajor=False, c=[C.data_ptr()],
+                     ldc=64, dbias_tab=[torch.zeros(64, device=DEV)], device=DEV)
+    finally:
+        lib.jmt_gemm_set_debug(0)
