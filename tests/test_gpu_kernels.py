@@ -818,8 +818,9 @@ def test_fused_attention_bwd_keymajor_handoff(Lq, Lk, N):
 @pytest.mark.parametrize("dsum", [False, True])
 @pytest.mark.parametrize("cd", [torch.bfloat16, torch.float32])
 def test_layernorm_grouped_equals_per_group(dsum, cd):
-    """jmt_layernorm_{fwd,bwd}_grouped (G groups, one launch each + one reduce) give bitwise the
-    per-group jmt_layernorm_fwd / _bwd(_dsum) results: same kernels, same partial-sum order."""
+    """jmt_layernorm_{fwd,bwd}_grouped (G groups, one launch each + one reduce) give the per-group
+    jmt_layernorm_fwd / _bwd(_dsum) results: forward and dx bitwise (same row math), the column
+    sums (dgamma, dbeta, dsum) to fp32 reassociation."""
     G, rows, D = 3, 1900, 512
     g = torch.Generator(device=DEV).manual_seed(37)
     X = torch.randn(G, rows, D, device=DEV, generator=g).to(cd)
@@ -857,10 +858,13 @@ def test_layernorm_grouped_equals_per_group(dsum, cd):
         outs.append((dX, dg, db, ds))
     (a, b) = outs
     assert torch.equal(a[0], b[0])
+    # the grouped launch folds 32 rows per partial (one group: 16): the same fp32 sums in a
+    # different association
+    close = lambda u, v: torch.allclose(u, v, rtol=1e-5, atol=1e-4)
     for i in range(G):
-        assert torch.equal(a[1][i], b[1][i]) and torch.equal(a[2][i], b[2][i])
+        assert close(a[1][i], b[1][i]) and close(a[2][i], b[2][i])
         if dsum:
-            assert torch.equal(a[3][i], b[3][i])
+            assert close(a[3][i], b[3][i])
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 5, 10, 11, 20, 21])
