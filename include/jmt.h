@@ -83,7 +83,8 @@ typedef struct jmt_gemm_desc {
   /* ABI 4: A row sums — the bias gradient of a weight-gradient GEMM dW = dY^T X, db[m] =
    * sum_k A[m][k] = the column sums of dY (nn.Linear's bias.grad, autograd of the same
    * modules) — taken from the A fragments inside the GEMM instead of a second pass over dY:
-   * when n_dbias > 0, dbias_tab[b0][m] (+)= (dbias_acc) the row sums of A[b0] (fp32).  16-bit
+   * when n_dbias > 0, dbias_tab[b0][m] (+)= (dbias_acc) the row sums of A[b0] (fp32; a NULL
+   * entry skips b0 — the segments of a K-concatenated wgrad share one dY).  16-bit
    * MN-major A and B, fp32 C, batch1 = 1; split-K needs dbias_ws (splits * batch0 * M floats). */
   float* dbias_tab[8];
   int n_dbias;

@@ -58,7 +58,7 @@ int main() {
   d.M = 128; d.a[0] = d.b[0] = d.c[0] = (void*)buf; d.c_dtype = JMT_F32;
   d.a_kmajor = 0; d.b_kmajor = 0; d.n_dbias = 1; d.dbias_tab[0] = nullptr;
   expect_err("gemm dbias null entry", jmt_gemm(&d, nullptr));
-  expect_msg("gemm dbias null entry", "dbias_tab");
+  expect_msg("gemm dbias null entry", "every dbias_tab entry");
   d.dbias_tab[0] = (float*)buf; d.a_kmajor = 1;
   expect_err("gemm dbias K-major A", jmt_gemm(&d, nullptr));
   expect_msg("gemm dbias K-major A", "row sums");

@@ -884,10 +884,11 @@ void gemm_kernel(GemmParams p) {
   [[maybe_unused]] const int wnu = __builtin_amdgcn_readfirstlane(wn);
   if constexpr (RS) {
     const int tn = cur.n0 / C::BN;
+    const bool want = p.dbias_tab[cur.b0] != nullptr;
     uint32_t own = 0;
 #pragma unroll
     for (int i = 0; i < C::TM; ++i)
-      if (i % C::WN == wnu && (i / C::WN) % p.tiles_n == tn) own |= 1u << i;
+      if (want && i % C::WN == wnu && (i / C::WN) % p.tiles_n == tn) own |= 1u << i;
     rsum.own = own;
 #pragma unroll
     for (int v = 0; v < RSumT::NV; ++v) rsum.v[v] = 0.f;
@@ -1054,7 +1055,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
       }
     }
     const int b0 = b / p.batch1, b1 = b % p.batch1;
-    if (p.n_dbias > 0 && n == 0) {   // the A row sums' split partials, in split order
+    if (p.n_dbias > 0 && n == 0 && p.dbias_tab[b0]) {   // the A row sums' split partials
       const float* src = p.dbias_ws + (int64_t)b * p.M + m;
       float r = 0.f;
       for (int t = 0; t < p.splits; ++t) r += src[(int64_t)t * nb * p.M];
@@ -1347,8 +1348,9 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
                       batch1 == 1 && d->n_dbias >= batch0,
                   "jmt_gemm: A row sums need 16-bit MN-major A and B, fp32 C, batch1 = 1 and a "
                   "dbias table of batch0 entries");
-    for (int i = 0; i < batch0; ++i)
-      JMT_CHECK_ARG(d->dbias_tab[i] != nullptr, "jmt_gemm: null dbias_tab[%d]", i);
+    bool any = false;   // null entries: no row sums for that batch entry (a K-concatenated
+    for (int i = 0; i < batch0; ++i) any = any || d->dbias_tab[i] != nullptr;   // wgrad's segments
+    JMT_CHECK_ARG(any, "jmt_gemm: every dbias_tab entry is null");
   }
   {
     const int ces = dtype_size(d->c_dtype);

@@ -262,17 +262,18 @@ def fused_bgrad_ok(cd) -> bool:
 def _wgrad(G: Rows, n, xin, ld_in, kseg, W, r0, cd, b=None) -> bool:
     """W.grad[r0:r0+n, s*kseg:...] += dY^T X_s   (split-K over the rows); with `b`, also
     b.grad[r0:r0+n] += the column sums of dY inside the same GEMM when the launch form allows it
-    (one K segment, n > 1, 16-bit).  Returns True when b.grad was written."""
+    (n > 1, 16-bit; K segments share dY, so only segment 0 sums it).  Returns True when b.grad
+    was written."""
     gW = _grad_buffer(W)
     if gW is None:
         return False
     nseg = len(xin)
     Kin = W.shape[1]
     dbt = None
-    if b is not None and n > 1 and nseg == 1 and fused_bgrad_ok(cd):
+    if b is not None and n > 1 and fused_bgrad_ok(cd):
         gb = _grad_buffer(b)
         if gb is not None:
-            dbt = [gb[r0:r0 + n]]
+            dbt = [gb[r0:r0 + n]] + [None] * (nseg - 1)
     # A = dY^T (MN-major); for n == 1 the single row is the contiguous dY column (K-major)
     a_ld, a_kmaj = (G.ld, False) if n > 1 else (_vec(cd), True)
     ops.gemm(M=n, N=kseg, K=G.rows, ab_dtype=_dc(cd), c_dtype=F32,
@@ -604,19 +605,22 @@ class MLPPairFn(Function):
         for W in W1s:
             g = _grad_buffer(W)
             gws.append(g if g is not None else torch.zeros_like(W))
-        ops.gemm(M=hid, N=L.F, K=L.rows, ab_dtype=_dc(cd), c_dtype=F32,
-                 a=[dh.data_ptr()], lda=ldh, a_kmajor=False,
-                 b=[xin.data_ptr()], ldb=L.ld, b_kmajor=False,
-                 c=[g.data_ptr() for g in gws], ldc=L.F, c_mode=1, batch0=2,
-                 sA=(hid, 0), sB=(0, 0), beta=1.0, device=dev)
-        _grad_done(*W1s)
         dbs = []
         for b in b1s:
             gb = _grad_buffer(b)
             dbs.append(gb if gb is not None else torch.empty(hid, dtype=torch.float32,
                                                              device=dev))
-        ops.colsum_grouped(dh.data_ptr(), _dc(cd), 2, ldh, hid, L.rows, hid, dbs,
-                           beta_acc=True, device=dev)
+        fuse = hid > 1 and fused_bgrad_ok(cd)      # bias sums as the wgrad's A row sums
+        ops.gemm(M=hid, N=L.F, K=L.rows, ab_dtype=_dc(cd), c_dtype=F32,
+                 a=[dh.data_ptr()], lda=ldh, a_kmajor=False,
+                 b=[xin.data_ptr()], ldb=L.ld, b_kmajor=False,
+                 c=[g.data_ptr() for g in gws], ldc=L.F, c_mode=1, batch0=2,
+                 sA=(hid, 0), sB=(0, 0), beta=1.0, dbias_tab=dbs if fuse else None,
+                 device=dev)
+        _grad_done(*W1s)
+        if not fuse:
+            ops.colsum_grouped(dh.data_ptr(), _dc(cd), 2, ldh, hid, L.rows, hid, dbs,
+                               beta_acc=True, device=dev)
         _grad_done(*b1s)
 
 

@@ -206,8 +206,8 @@ class StackJointFn(Function):
         dX = _contig(dX, cd)
         G = Rows(dX[2])
         _dgrad(G, E, W, 0, cd, [dX[0], dX[1]], E, 2, E, beta=1.0)
-        _wgrad(G, E, [X[0], X[1]], E, E, W, 0, cd)
-        _bgrad(G, E, b, 0)
+        if not _wgrad(G, E, [X[0], X[1]], E, E, W, 0, cd, b):
+            _bgrad(G, E, b, 0)
         dv = dX[0] if vdt == cd else _cast_keep_layout(dX[0], vdt)
         dp = dX[1] if pdt == cd else _cast_keep_layout(dX[1], pdt)
         return dv, dp, None, None
@@ -737,16 +737,23 @@ class ConcatLinearFn(Function):
                  c=[dX.data_ptr()], ldc=E, sC=(R * E, 0), batch0=S, device=dev)
 
         def param_grads():      # side stream: overlaps the dgrads of the cross-attentions
+            from .functional import fused_bgrad_ok
             gW = _grad_buffer(W)
+            gb = _grad_buffer(b)
+            fuse = gW is not None and gb is not None and N > 1 and fused_bgrad_ok(cd)
             if gW is not None:
+                # the S K-segments share dY: segment 0 also takes its row sums (the bias grad)
                 ops.gemm(M=N, N=E, K=R, ab_dtype=_dc(cd), c_dtype=ops.F32,
                          a=[dy.data_ptr()], lda=N, a_kmajor=False, sA=(0, 0),
                          b=[X.data_ptr()], ldb=E, b_kmajor=False, sB=(R * E, 0),
                          c=[gW.data_ptr()], ldc=S * E, sC=(E, 0), batch0=S, beta=1.0,
-                         device=dev)
+                         dbias_tab=[gb] + [None] * (S - 1) if fuse else None, device=dev)
                 _grad_done(W)
             if b is not None:
-                _bias_grad(dy, N, R, N, b, 0)
+                if fuse:
+                    _grad_done(b)
+                else:
+                    _bias_grad(dy, N, R, N, b, 0)
 
         streams.run_side(param_grads, reads=(dy, X))
         return dX, None, None

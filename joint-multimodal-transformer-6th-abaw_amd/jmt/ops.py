@@ -63,8 +63,8 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
          bias_mode: int = 1, relu: bool = False, aux: Optional[torch.Tensor] = None,
          ldaux: int = 0, splits: Optional[int] = None, bias_tab=None, dbias_tab=None,
          dbias_acc: bool = True, device=None) -> None:
-    """dbias_tab: per-b0 fp32 outputs that receive (dbias_acc: += ) the row sums of A — a
-    weight-gradient GEMM's bias gradient (jmt_gemm_desc ABI 4)."""
+    """dbias_tab: per-b0 fp32 outputs (None: skip that entry) that receive (dbias_acc: += ) the
+    row sums of A — a weight-gradient GEMM's bias gradient (jmt_gemm_desc ABI 4)."""
     d = GemmDesc()
     d.ab_dtype, d.c_dtype = ab_dtype, c_dtype
     d.aux_dtype = dt(aux) if aux is not None else c_dtype
@@ -99,7 +99,7 @@ def gemm(*, M: int, N: int, K: int, ab_dtype: int, c_dtype: int,
     ws = None
     if dbias_tab:
         for i, t in enumerate(dbias_tab):
-            d.dbias_tab[i] = t.data_ptr()
+            d.dbias_tab[i] = t.data_ptr() if t is not None else None
         d.n_dbias = len(dbias_tab)
         d.dbias_acc = int(dbias_acc)
     if splits > 1:

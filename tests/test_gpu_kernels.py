@@ -907,6 +907,20 @@ def test_gemm_wgrad_row_sums_bias_grad(cfg, dt):
                 err = (db[i] - ref).abs().max().item()
                 scale = dY[i, :, :n].float().abs().sum(0).max().item()
                 assert err <= 1e-6 * scale + 1e-5, (cfg, n, Kin, rows, splits, i, err)
+        # K-concatenated wgrad: the segments share dY (sA = 0), only segment 0 takes the sums
+        n, Kin, rows = 512, 256, 3000
+        dY = torch.randn(rows, n, device=DEV, generator=g).to(t)
+        X = torch.randn(2, rows, Kin, device=DEV, generator=g).to(t)
+        C = torch.zeros(n, 2 * Kin, device=DEV)
+        db = torch.randn(n, device=DEV, generator=g)
+        db0 = db.clone()
+        ops.gemm(M=n, N=Kin, K=rows, ab_dtype=dt, c_dtype=F32, a=[dY.data_ptr()], lda=n,
+                 a_kmajor=False, sA=(0, 0), b=[X.data_ptr()], ldb=Kin, b_kmajor=False,
+                 sB=(rows * Kin, 0), c=[C.data_ptr()], ldc=2 * Kin, sC=(Kin, 0), batch0=2,
+                 beta=1.0, dbias_tab=[db, None], device=DEV)
+        torch.cuda.synchronize()
+        ref = db0 + dY.float().sum(0)
+        assert (db - ref).abs().max().item() <= 1e-6 * dY.float().abs().sum(0).max().item() + 1e-5
         with pytest.raises(_lib.JMTError):    # K-major A: not a weight-gradient launch
             A = torch.randn(64, 64, device=DEV).to(t)
             C = torch.empty(64, 64, device=DEV)
