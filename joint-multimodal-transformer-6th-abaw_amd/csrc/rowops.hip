@@ -5,6 +5,9 @@
 // fp32 partial slabs + a second pass (deterministic, no atomics).
 #include "common.h"
 
+#include <cstdlib>
+#include <type_traits>
+
 namespace jmt {
 
 constexpr int RB = 256;   // threads per block (4 waves)
@@ -171,6 +174,41 @@ __global__ __launch_bounds__(RB) void l2norm_fwd_vec_kernel(int64_t rows, const 
     V4<TY>::st(y + r * ldy + 4 * (lane + 64 * j), o);
   }
   if (lane == 0) inv_norm[r] = inv;
+}
+
+// single-pass backward (D = 256 NV, 4-element aligned rows): x and dy are read once, 8-B / 16-B
+// per lane, and kept in registers between the row dot product and the write (the loop form above
+// reads both twice with 2-B lane loads)
+template <typename TX, typename TG, typename TD, int NV>
+__global__ __launch_bounds__(RB) void l2norm_bwd_vec_kernel(int64_t rows, const TX* x,
+                                                            int64_t ldx, const TG* dy,
+                                                            int64_t lddy, const float* inv_norm,
+                                                            float eps, TD* dx, int64_t lddx) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float inv = inv_norm[r];
+  const bool clamped = !(inv < 1.f / eps);
+  float xv[NV][4], gv[NV][4];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    V4<TX>::ld(x + r * ldx + 4 * (lane + 64 * j), xv[j]);
+    V4<TG>::ld(dy + r * lddy + 4 * (lane + 64 * j), gv[j]);
+  }
+  float dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dot += xv[j][e] * inv * gv[j][e];
+  dot = wave_sum(dot);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      o[e] = clamped ? gv[j][e] * inv : (gv[j][e] - xv[j][e] * inv * dot) * inv;
+    V4<TD>::st(dx + r * lddx + 4 * (lane + 64 * j), o);
+  }
 }
 
 // Grouped LayerNorm (round 3): G same-shaped LayerNorms (the grouped encoders' LN1 / LN2, one per
@@ -749,10 +787,24 @@ extern "C" int jmt_l2norm_bwd(int x_dt, int dy_dt, int dx_dt, int64_t rows, int 
   if (rows == 0) return JMT_OK;
   JMT_CHECK_ARG(D > 0 && x && dy && dx && inv_norm, "jmt_l2norm_bwd: bad args");
   hipStream_t st = as_stream(stream);
+  const bool vec = (D == 512 || D == 1024 || D == 2048) && ldx % 4 == 0 && lddy % 4 == 0 &&
+                   lddx % 4 == 0 && ((uintptr_t)x % (4 * dtype_size(x_dt))) == 0 &&
+                   ((uintptr_t)dy % (4 * dtype_size(dy_dt))) == 0 &&
+                   ((uintptr_t)dx % (4 * dtype_size(dx_dt))) == 0;
+#define JMT_L2BV(NV)                                                                          \
+  hipLaunchKernelGGL((l2norm_bwd_vec_kernel<TX, TG, TD, NV>), dim3(row_blocks(rows)), dim3(RB), \
+                     0, st, rows, (const TX*)x, ldx, (const TG*)dy, lddy, inv_norm, eps,       \
+                     (TD*)dx, lddx)
   JMT_DISPATCH1(x_dt, TX, JMT_DISPATCH1(dy_dt, TG, JMT_DISPATCH1(dx_dt, TD,
-      hipLaunchKernelGGL((l2norm_bwd_kernel<TX, TG, TD>), dim3(row_blocks(rows)), dim3(RB), 0, st,
-                         rows, D, (const TX*)x, ldx, (const TG*)dy, lddy, inv_norm, eps, (TD*)dx,
-                         lddx))));
+      if (vec && D == 512) { JMT_L2BV(2); }
+      else if (vec && D == 1024) { JMT_L2BV(4); }
+      else if (vec && D == 2048) { JMT_L2BV(8); }
+      else {
+        hipLaunchKernelGGL((l2norm_bwd_kernel<TX, TG, TD>), dim3(row_blocks(rows)), dim3(RB), 0,
+                           st, rows, D, (const TX*)x, ldx, (const TG*)dy, lddy, inv_norm, eps,
+                           (TD*)dx, lddx);
+      })));
+#undef JMT_L2BV
   JMT_LAUNCH_CHECK("jmt_l2norm_bwd");
   return JMT_OK;
 }
@@ -1071,13 +1123,25 @@ extern "C" int jmt_layernorm_bwd_grouped(int dt_in, int dt_dy, int dt_dx, int G,
   hipStream_t st = as_stream(stream);
   const int nblk = (int)((rows + LN_ROWS_PER_BLOCK_GROUPED - 1) / LN_ROWS_PER_BLOCK_GROUPED);
   const dim3 grid((unsigned)nblk, (unsigned)G);
-#define JMT_LNBG(NV, DS)                                                                         \
-  hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV, DS, LN_ROWS_PER_BLOCK_GROUPED, 2>), grid, \
+  // development A/B: rows in flight per wave (JMT_LN_BWD_U=4; D = 512, one dtype throughout)
+  static const int ln_u = [] {
+    const char* e = getenv("JMT_LN_BWD_U");
+    return (e && atoi(e) == 4) ? 4 : 2;
+  }();
+#define JMT_LNBG_U(NV, DS, U)                                                                    \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV, DS, LN_ROWS_PER_BLOCK_GROUPED, U>), grid, \
                      dim3(RB), 0, st, rows,                                                     \
                      (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd,     \
                      grp.gamma[0], (TD*)dx, lddx, partials, grp)
+#define JMT_LNBG(NV, DS) JMT_LNBG_U(NV, DS, 2)
   JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_dy, TG, JMT_DISPATCH1(dt_dx, TD,
-      if (dsum) {
+      constexpr bool same = sizeof(TI) == 2 && std::is_same<TI, TG>::value &&
+                            std::is_same<TI, TD>::value;
+      if (same && ln_u == 4 && D == 512) {
+        if constexpr (same) {
+          if (dsum) { JMT_LNBG_U(2, true, 4); } else { JMT_LNBG_U(2, false, 4); }
+        }
+      } else if (dsum) {
         if (D == 512) { JMT_LNBG(2, true); }
         else if (D == 768) { JMT_LNBG(3, true); }
         else { JMT_LNBG(4, true); }
@@ -1087,6 +1151,7 @@ extern "C" int jmt_layernorm_bwd_grouped(int dt_in, int dt_dy, int dt_dx, int G,
         else { JMT_LNBG(4, false); }
       })));
 #undef JMT_LNBG
+#undef JMT_LNBG_U
   JMT_LAUNCH_CHECK("jmt_layernorm_bwd_grouped");
   const int NS = dsum ? 3 : 2;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((NS * D + 15) / 16, G), dim3(RB), 0, st, nblk,

@@ -210,9 +210,10 @@ def test_gemm_large_bf16_linear_shape():
 
 
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
-def test_l2norm_fwd_bwd(cd):
+@pytest.mark.parametrize("D", [2048, 512, 768])      # vector kernels (NV 8, 2) and the loop form
+def test_l2norm_fwd_bwd(cd, D):
     g = torch.Generator(device=DEV).manual_seed(6)
-    x = torch.randn(5, 37, 2048, device=DEV, generator=g)
+    x = torch.randn(5, 37, D, device=DEV, generator=g)
     x[0, 0] = 0.0                                      # the eps-clamped branch
     x.requires_grad_(True)
     with JF.compute_mode(cd):
