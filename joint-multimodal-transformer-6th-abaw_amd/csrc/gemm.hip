@@ -1204,13 +1204,17 @@ static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, in
   // 45 -> 36, K-concat stream dgrad 94 -> 84 (was Cfg11); and the grouped qkv forward (b3,
   // N = 1536) 167 -> 161.  Batched N = 512 / 1024 launches stay on 256x256 (cfg 30 lost 6-15 %
   // there: 1.76 / 3.5 waves already quantise well).  profiles/r03_gemm_tile160.jsonl
-  if (splits <= 1 && ak && M >= 4096 && K >= 512 && K % 64 == 0 &&
+  // These B*T-row overrides were measured at c3's 19,200 rows; at c2's 9,600 the planner's own
+  // tile is faster (video linear fwd 51.5 -> 35.8 us, FcLayer fwd 30.5 -> 23.6, head dgrad 30.8
+  // -> 24.5, K-concat stream dgrad 80.1 -> 66.7, qkv fwd b3 97.2 -> 77.1, qkv wgrad b3 101 ->
+  // 81: profiles/r03_c2_gemm_tiles.jsonl), so they are keyed to >= 16,384 rows.
+  if (splits <= 1 && ak && M >= 16384 && K >= 512 && K % 64 == 0 &&
       ((batch == 1 && N <= 1024) || (bk && batch == 3 && N == 1536 && K == 512)))
     return 30;
   // the stacked-stream dgrad of out_layer_pv (b2, beta = 1): 65 -> 57 us (1.17 waves of 256x256
   // tiles, 1.88 of 160x256; profiles/r03_nn_sweep.jsonl)
   if (splits <= 1 && ak && !bk && batch == 2 && M >= 4096 && N == 512 && K == 512) return 30;
-  if (!ak && !bk && M >= 1536 && N >= 512 && batch >= 3 && K >= 8192)
+  if (!ak && !bk && M >= 1536 && N >= 512 && batch >= 3 && K >= 16384)
     return 10;                                                   // split-K qkv wgrad
   if (!ak && !bk && batch == 6 && M == 1024 && N == 512 && K >= 8192)
     return 5;          // cross-attention k|v wgrad: 256x256 at the planner's splits (-8 %,
@@ -1218,7 +1222,7 @@ static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, in
   if (splits > 1) return 0;
   if (!ak && !bk && batch >= 64 && M <= 512 && N <= 512 && K >= 128 && K <= 512)
     return 11;                                                   // attn dK / dV
-  if (ak && !bk && batch == 1 && K >= 3072) return 11;           // K-concat stream dgrad
+  if (ak && !bk && batch == 1 && K >= 3072 && M >= 16384) return 11;   // K-concat stream dgrad
   if (ak && !bk && batch == 1 && K <= 128 && M >= 4096 && N >= 512)
     return 11;         // short-K dgrad (the regressors' first layer, K = 128): 28.7 -> 23.3 us,
                        // profiles/r02_regressor_gemm_sweep.jsonl
