@@ -14,6 +14,7 @@ Requirements the JMT path meets by construction:
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional
 
 import torch
@@ -39,7 +40,11 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # JMT_COMPUTE_PRIO=1: capture on a high-priority stream, so the step's critical chain
+        # outranks the weight-gradient side stream (jmt.streams, default priority) when both
+        # have blocks waiting for CUs
+        cap = torch.cuda.Stream(priority=-1) if os.environ.get("JMT_COMPUTE_PRIO") == "1" else None
+        with torch.cuda.graph(self.graph, stream=cap):
             self.out = self.step_fn()
         torch.cuda.synchronize()
         return self

@@ -195,6 +195,67 @@ def test_gemm_kconcat_and_pointer_tables(dt):
     assert (dW - ref).abs().max().item() <= _tol(dt, M) * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("cfg", [40, 41])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_persistent(cfg, ak, bk):
+    """gemm_persist_kernel (csrc/gemm_persist.hip: one block per CU walks whole 256x256 tiles
+    with one LDS-DMA pipeline across tile boundaries, stores drained under the next tile's
+    MFMAs) vs torch fp32: more tiles than CUs (2-4 tiles per block, uneven), batched with bias
+    tables, a K-concatenated A, C pointer tables, ReLU / alpha / per-column bias, K down to two
+    K-tiles (the store window then spans a whole tile); and dbg 32 (every wait also drains the
+    last epilogue's stores) bit-identical."""
+    from jmt import _lib
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(40)
+    bf = torch.bfloat16
+
+    def run(**kw):
+        out = []
+        for dbg in (0, 32):
+            lib.jmt_gemm_set_debug((cfg << 8) | dbg)
+            try:
+                ops.gemm(device=DEV, **{k: v for k, v in kw.items() if k != "c"},
+                         c=[t.data_ptr() for t in kw["c"]])
+            finally:
+                lib.jmt_gemm_set_debug(0)
+            out.append([t.clone() for t in kw["c"]])
+        for a, b in zip(*out):
+            assert torch.equal(a, b), "dbg 32 (stores drained at every wait) changed the result"
+        return out[0]
+
+    for (M, N, K, nb) in [(10240, 512, 256, 4), (512, 1536, 128, 3), (2304, 256, 512, 1)]:
+        A, Al, lda, sa = _operand(M, K, ak, BF16, batch=nb, gen=g)
+        Bs, Bl_t, ldb, sb = _operand(N, K, bk, BF16, batch=nb, gen=g)
+        Bl = Bl_t.transpose(1, 2)
+        bias = [torch.randn(N, device=DEV, generator=g) for _ in range(nb)]
+        C = torch.empty(nb, M, N, device=DEV, dtype=bf)
+        (C2,) = run(M=M, N=N, K=K, ab_dtype=BF16, c_dtype=BF16, a=[A.data_ptr()], lda=lda,
+                    a_kmajor=ak, sA=(sa, 0), b=[Bs.data_ptr()], ldb=ldb, b_kmajor=bk,
+                    sB=(sb, 0), c=[C], ldc=N, sC=(M * N, 0), batch0=nb, alpha=0.75,
+                    bias_tab=bias, bias_mode=1, relu=True, splits=1)
+        for i in range(nb):
+            ref = torch.relu(0.75 * (Al[i] @ Bl[i]) + bias[i])
+            err = (C2[i].float() - ref).abs().max().item()
+            assert err <= 1e-2 * ref.abs().max().item(), (cfg, M, N, K, i, err)
+    if ak:
+        # K-concat A (4 segments of 128) x (K-major | MN-major) B into a C pointer table of two
+        # (batch1-strided) outputs, one bias for every batch entry
+        M, N, seg = 1536, 512, 128
+        As = [torch.randn(M, seg, device=DEV, generator=g).to(bf) for _ in range(4)]
+        Bs2, Bl_t2, ldb2, sb2 = _operand(N, 4 * seg, bk, BF16, batch=2, gen=g)
+        bias = torch.randn(N, device=DEV, generator=g)
+        outs = [torch.empty(M, N, device=DEV, dtype=bf) for _ in range(2)]
+        res = run(M=M, N=N, K=4 * seg, ab_dtype=BF16, c_dtype=BF16, a=[a.data_ptr() for a in As],
+                  lda=seg, a_kmajor=True, a_mode=2, a_kseg=seg, b=[Bs2.data_ptr()], ldb=ldb2,
+                  b_kmajor=bk, sB=(sb2, 0), c=outs, c_mode=1, ldc=N, batch0=2, bias=bias,
+                  bias_mode=1, splits=1)
+        Acat = torch.cat([a.float() for a in As], 1)
+        for i in range(2):
+            ref = Acat @ Bl_t2.transpose(1, 2)[i] + bias
+            err = (res[i].float() - ref).abs().max().item()
+            assert err <= 1e-2 * ref.abs().max().item(), (cfg, "kcat", i, err)
+
+
 def test_gemm_large_bf16_linear_shape():
     """The benchmark's dominant shape: (19200 x 1024) @ (1024 x 512)^T in bf16."""
     g = torch.Generator(device=DEV).manual_seed(5)
