@@ -298,6 +298,9 @@ def main():
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--parity-perturb", type=float, default=0.0,
+                    help="scale cross_attention_v.out_proj.weight by 1+x before the parity check "
+                         "(shows that the check fails)")
     ap.add_argument("--no-probe", action="store_true", help="no per-launch events (profiling)")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="replay the whole step as one hipGraph (default)")
@@ -401,20 +404,27 @@ def main():
     # state lives on the device, so the step stays one graph replay
     scaler = GradScaler(device=dev) if cd == torch.float16 else None
 
+    # train.py:309-314: v_loss + a_loss summed by the second criterion's finish kernel
+    # (CCCLoss.forward_add), backward seeded with a persistent 1 — the step runs no torch kernel
+    one = torch.ones((), dtype=torch.float32, device=dev)
+
     def fwd_bwd():
         with JF.compute_mode(cd):
             vo, ao = model(fc(audio) if fc is not None else audio, video)
             l1 = crit(flat(vo), lv)
-            l2 = crit(flat(ao), la)
-            loss = l1 + l2
-            (scaler.scale(loss) if scaler is not None else loss).backward()
+            loss = crit.forward_add(flat(ao), la, l1)
+            if scaler is not None:
+                scaler.scale(loss).backward()
+            else:
+                loss.backward(one)
         return loss
 
     # the parameters that get a gradient, laid out in the order their gradients complete, so
     # that the all-reduce buckets become ready one after another during the backward
     params, wcounts = jdist.grad_write_profile(fwd_bwd, list(model.parameters()) +
                                                (list(fc.parameters()) if fc is not None else []))
-    opt = FusedSGD(params, **sgd_kw, shadow_dtype=cd if cd != torch.float32 else None)
+    opt = FusedSGD(params, **sgd_kw, shadow_dtype=cd if cd != torch.float32 else None,
+                   fuse_zero_grad=True)
     bucketer = None
     if world > 1 and not args.no_overlap:
         bucketer = jdist.GradBucketer(opt, wcounts, bucket_bytes=args.bucket_mb << 20,
@@ -556,8 +566,26 @@ def main():
 
     parity = None
     if rank == 0 and not args.no_parity:
-        parity = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv,
-                              k=k, H=heads, L=layers)
+        if (cfg["jm"], cfg["fmt"], cfg["fc"], k, heads, layers, Dv, Da) == \
+                ("TRANSFORMER", "FC", True, 1, 1, 1, 2048, 1024) and cd != torch.float32 and \
+                T == 300 and B >= 4:
+            # discriminative form: conditioned weights, the bench shape,
+            # every parameter gradient under the strict 16-bit bound (tests/parity.py)
+            from tests.parity import window_subset_check
+            torch.set_num_threads(cpu_threads()[0])
+            win = (0, B // 3, (2 * B) // 3, B - 1)
+            parity = window_subset_check(cd, B=B, T=T, win=win, perturb=args.parity_perturb)
+            parity["reference"] = ("oracle/jmt_ref.py fp32 CPU on windows %s of a B=%d T=%d batch "
+                                   "(whole batch on the GPU), conditioned hash-init weights, "
+                                   "objective zero outside those windows" % (list(win), B, T))
+            parity["tolerance"] = ("min(5 %, 4 x the rounding-emulating oracle's error, floor "
+                                   "2u) per prediction set / parameter gradient")
+            if args.parity_perturb:
+                parity["perturbed"] = ("cross_attention_v.out_proj.weight x %g on the GPU"
+                                       % (1 + args.parity_perturb))
+        else:
+            parity = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv,
+                                  k=k, H=heads, L=layers)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3" and \
             jcfg is None:

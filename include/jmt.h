@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define JMT_ABI_VERSION 4
+#define JMT_ABI_VERSION 5
 
 enum { JMT_F32 = 0, JMT_BF16 = 1, JMT_F16 = 2 };
 enum { JMT_OK = 0, JMT_ERR_ARG = -1, JMT_ERR_HIP = -2, JMT_ERR_UNSUPPORTED = -3 };
@@ -311,6 +311,11 @@ int jmt_ccc_stats(int kind, int pred_dt, int64_t n, int k, const void* pred, con
                   float ignore, float lo, float hi, double* stats, void* stream);
 int jmt_ccc_finish(int kind, int world, const double* stats_all, int64_t bs, float eps,
                    float* loss, double* coef, void* stream);
+/* ABI 5: the same, writing *add + loss (one fp32 rounding, as torch's l1 + l2 of
+ * train.py:311) when add != NULL: the two criteria of a training step summed in the finish
+ * kernel instead of a separate add launch. */
+int jmt_ccc_finish_add(int kind, int world, const double* stats_all, int64_t bs, float eps,
+                       const float* add, float* loss, double* coef, void* stream);
 int jmt_ccc_bwd(int kind, int pred_dt, int64_t n, int k, const void* pred, const float* label,
                 float ignore, float lo, float hi, const double* coef, const float* grad_loss,
                 void* dpred, void* stream);
@@ -342,6 +347,11 @@ int jmt_mask_indices(int64_t n, const float* label, float ignore, int64_t* idx, 
 int jmt_sgd_step(int64_t n, float* param, const float* grad, float* momentum_buf, float lr,
                  float momentum, float dampening, float weight_decay, int nesterov,
                  int first_step, float grad_scale, void* shadow, int shadow_dt, void* stream);
+/* ABI 5: the same step, then grad[i] = 0 in the same pass (the next step's optimizer.zero_grad()
+ * folded into this kernel; for jmt_sgd_step_amp_zero also on a skipped, found_inf step). */
+int jmt_sgd_step_zero(int64_t n, float* param, float* grad, float* momentum_buf, float lr,
+                      float momentum, float dampening, float weight_decay, int nesterov,
+                      int first_step, float grad_scale, void* shadow, int shadow_dt, void* stream);
 
 /* GradScaler with device-resident state (train.py:89,314-316): amp[5] fp32 = {scale, inv_scale,
  * found_inf, growth_tracker, steps_taken}.  jmt_amp_check sets found_inf if any grad*inv_scale is
@@ -353,6 +363,10 @@ int jmt_sgd_step_amp(int64_t n, float* param, const float* grad, float* momentum
                      float momentum, float dampening, float weight_decay, int nesterov,
                      int allow_first, const float* amp, void* shadow, int shadow_dt,
                      void* stream);
+int jmt_sgd_step_amp_zero(int64_t n, float* param, float* grad, float* momentum_buf, float lr,
+                          float momentum, float dampening, float weight_decay, int nesterov,
+                          int allow_first, const float* amp, void* shadow, int shadow_dt,
+                          void* stream);
 int jmt_amp_update(float* amp, float growth_factor, float backoff_factor, int growth_interval,
                    void* stream);
 

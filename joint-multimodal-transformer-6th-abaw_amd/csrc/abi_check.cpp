@@ -110,6 +110,8 @@ int main() {
   expect_err("ccc_stats bins", jmt_ccc_stats(0, JMT_F32, 10, 100, misal, fnull, 0.f, -1.f, 1.f,
                                              (double*)buf, nullptr));
   expect_err("ccc_finish null", jmt_ccc_finish(0, 0, nullptr, 1, 1e-8f, fnull, nullptr, nullptr));
+  expect_err("ccc_finish_add null", jmt_ccc_finish_add(0, 1, nullptr, 1, 1e-8f, fnull, fnull,
+                                                       nullptr, nullptr));
   expect_err("ce_stats bins", jmt_ce_stats(JMT_F32, 10, 1, misal, fnull, -1.f, 1.f, fnull,
                                            (double*)buf, nullptr));
   expect_err("ce_bwd null", jmt_ce_bwd(JMT_F32, 10, 5, nullptr, fnull, -1.f, 1.f, fnull, nullptr,
@@ -120,6 +122,11 @@ int main() {
   // optimizer, validation post-processing, feature store
   expect_err("sgd null", jmt_sgd_step(10, fnull, fnull, fnull, 0.1f, 0.9f, 0.f, 0.f, 1, 1, 1.f,
                                       nullptr, JMT_BF16, nullptr));
+  expect_err("sgd_zero null", jmt_sgd_step_zero(10, fnull, nullptr, fnull, 0.1f, 0.9f, 0.f, 0.f,
+                                                1, 1, 1.f, nullptr, JMT_BF16, nullptr));
+  expect_err("sgd_amp_zero null", jmt_sgd_step_amp_zero(10, fnull, fnull, fnull, 0.1f, 0.9f,
+                                                        0.f, 0.f, 1, 1, nullptr, nullptr,
+                                                        JMT_BF16, nullptr));
   expect_err("vp_ccc null", jmt_vp_ccc(10, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr));
   expect_err("gather null", jmt_gather_rows(JMT_F32, JMT_BF16, 4, 512, nullptr, 512, 4, nullptr,
                                             nullptr, 512, nullptr));

@@ -115,8 +115,8 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
     for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const F*)(qrow + 32 * ks);
   };
   load_q(n, hd, q0);
-  stage_rows<T, AF_KT>(kimg, kb, p.sk_l, 0, p.Lk);
-  stage_rows<T, AF_KT>(vimg, vb, p.sv_l, 0, p.Lk);
+  stage_rows<T, AF_KT, 8, true>(kimg, kb, p.sk_l, 0, p.Lk);
+  stage_rows<T, AF_KT, 8, true>(vimg, vb, p.sv_l, 0, p.Lk);
 
   f32x4* xmine = (f32x4*)(xch + w * AT_XCH) + lane;
   const f32x4* xpart = (const f32x4*)(xch + (w ^ 4) * AT_XCH) + lane;
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
       const T* kb_next = j + 1 < nkt ? kb : kb2;
       const int k0_next = j + 1 < nkt ? AF_KT * (j + 1) : 0;
       if constexpr ((OPT & 4) == 0) {
-        if (stage_k) stage_rows<T, AF_KT>(kimg, kb_next, p.sk_l, k0_next, p.Lk);
+        if (stage_k) stage_rows<T, AF_KT, 8, true>(kimg, kb_next, p.sk_l, k0_next, p.Lk);
       }
       if (j + 1 == nkt && more) load_q(n2, hd2, q02);   // next item's Q (registers free)
       const int kbase = AF_KT * j + 4 * g;
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
           if constexpr ((OPT & 4) != 0) {           // 2 of the 8 K-tile pieces per batch pair
             constexpr int NP = AF_KT / 8;
             if (stage_k)
-              stage_rows_part<T, AF_KT>(kimg, kb_next, p.sk_l, k0_next, p.Lk, (b / 2) * NP / 4,
+              stage_rows_part<T, AF_KT, 8, true>(kimg, kb_next, p.sk_l, k0_next, p.Lk, (b / 2) * NP / 4,
                                         (b / 2 + 1) * NP / 4);
             __builtin_amdgcn_sched_barrier(0);
           }
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
         wait_vmcnt<0>();                            // K tile j+1 landed
         stamp<STAMP>(p.stamps, 8 * j + 6);
         lds_barrier();                              // V image and exchange slots free
-        stage_rows<T, AF_KT>(vimg, vb, p.sv_l, AF_KT * (j + 1), p.Lk);
+        stage_rows<T, AF_KT, 8, true>(vimg, vb, p.sv_l, AF_KT * (j + 1), p.Lk);
       }
     }
     stamp<STAMP>(p.stamps, 254);
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
                         qr < p.Lq);
     if (!more) break;
     lds_barrier();                                  // every wave is done with the V image
-    stage_rows<T, AF_KT>(vimg, vb2, p.sv_l, 0, p.Lk);
+    stage_rows<T, AF_KT, 8, true>(vimg, vb2, p.sv_l, 0, p.Lk);
     item = nxt; nh = nh2; n = n2; hd = hd2; q0 = q02; kb = kb2; vb = vb2;
   }
 }

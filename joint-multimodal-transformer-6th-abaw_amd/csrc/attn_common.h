@@ -37,7 +37,12 @@ __device__ __forceinline__ void lds_barrier() {
 // Row addresses are wave-uniform (scalar arithmetic, saddr + 32-bit lane offset); the lane's
 // 16-B chunk is the swizzle of the image: LDS chunk `lane` of row r holds source chunk
 // lane ^ ((r & 7) << 1).
-template <typename T, int R, int NW = 8>
+// ASM: the DMA from inline asm (common.h glds16_asm, invisible to hipcc's wait bookkeeping).
+// The forward takes it: hipcc otherwise drains the next K tile before the P V phase's
+// transposed V reads (-4 % at L = 300, -9 % at L = 1024); the backward keeps the builtin: its
+// register loads of Q / dO are waited for by hipcc's own counts, which the hidden DMA would make
+// short (+5 %; profiles/r04/attn_glds_ab.txt).
+template <typename T, int R, int NW = 8, bool ASM = false>
 __device__ __forceinline__ void stage_rows(char* img, const T* base, int64_t ld, int k0, int Lk) {
   constexpr int NI = R / NW;
   const int lane = threadIdx.x & 63;
@@ -49,13 +54,14 @@ __device__ __forceinline__ void stage_rows(char* img, const T* base, int64_t ld,
     JMT_DCHECK(src >= 0 && src < Lk);
     const char* row = (const char*)(base + (int64_t)src * ld);
     const unsigned off = (unsigned)(lane ^ ((r & 7) << 1)) << 4;
-    glds16(row + off, img + r * AT_ROWB);
+    if constexpr (ASM) glds16_asm(row + off, img + r * AT_ROWB);
+    else glds16(row + off, img + r * AT_ROWB);
   }
 }
 
 // pieces [i0, i1) of stage_rows (the NI = R / NW wave-instructions of this wave), so the DMA of a
 // tile can be issued between the MFMA batches of a phase instead of in one burst
-template <typename T, int R, int NW = 8>
+template <typename T, int R, int NW = 8, bool ASM = false>
 __device__ __forceinline__ void stage_rows_part(char* img, const T* base, int64_t ld, int k0,
                                                 int Lk, int i0, int i1) {
   constexpr int NI = R / NW;
@@ -69,7 +75,8 @@ __device__ __forceinline__ void stage_rows_part(char* img, const T* base, int64_
     JMT_DCHECK(src >= 0 && src < Lk);
     const char* row = (const char*)(base + (int64_t)src * ld);
     const unsigned off = (unsigned)(lane ^ ((r & 7) << 1)) << 4;
-    glds16(row + off, img + r * AT_ROWB);
+    if constexpr (ASM) glds16_asm(row + off, img + r * AT_ROWB);
+    else glds16(row + off, img + r * AT_ROWB);
   }
 }
 

@@ -125,9 +125,12 @@ __global__ __launch_bounds__(CT) void ccc_stats_kernel(int kind, int64_t n, int 
 // bs (kind 1, CCCLoss.py:17 `y_pred.size(0)` before masking): bs >= 1 is used as given (the
 // (1, B*T) view of train.py:303-307: size(0) is 1 on every rank and after the gather); bs < 0
 // means "1-D predictions": size(0) of the GATHERED batch = the sum of the ranks' pre-mask counts.
+// `add` (may be NULL): the loss written is *add + this loss, rounded once as torch's fp32
+// `l1 + l2` of train.py:311 (the two criteria of a step summed without a separate add kernel)
 __global__ void ccc_finish_kernel(int kind, int world, const double* st, int64_t bs_in, float eps,
-                                  float* loss, double* coef) {
+                                  const float* add, float* loss, double* coef) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  auto put = [&](float v) { *loss = add ? *add + v : v; };
   double n = st[0], mx = st[1], my = st[2], Sxx = st[3], Syy = st[4], Sxy = st[5];
   double bsd = (double)bs_in;
   if (bs_in < 0) {
@@ -161,7 +164,7 @@ __global__ void ccc_finish_kernel(int kind, int world, const double* st, int64_t
     const float dmean = (float)mx - (float)my;
     const float den = xs * xs + ys * ys + dmean * dmean;
     const float ccc = 2.f * rho * xs * ys / den;
-    *loss = 1.f - ccc;
+    put(1.f - ccc);
     // analytic gradient in double
     const double nm1 = n - 1.0;
     const double A = sqrt(Sxx), Bv = sqrt(Syy), Q = A * Bv + (double)eps;
@@ -180,7 +183,7 @@ __global__ void ccc_finish_kernel(int kind, int world, const double* st, int64_t
     // losses/CCCLoss.py:24-43: masked compaction, <=1 element -> 0; std names swapped;
     // ccc = 2 s_xy / ((std(t)^2 + std(p)^2 + (mp - mt)^2 + 1e-8) * bs)
     if (n <= 1.0) {
-      *loss = 0.f;
+      put(0.f);
       return;
     }
     const float fn = (float)n;
@@ -189,7 +192,7 @@ __global__ void ccc_finish_kernel(int kind, int world, const double* st, int64_t
     const float dm = (float)mx - (float)my;
     const float den = x_std * x_std + y_std * y_std + dm * dm + 1e-8f;
     const float ccc = 2.f * (float)Sxy / (den * (float)bsd);
-    *loss = 1.f - ccc;
+    put(1.f - ccc);
     const double nm1 = n - 1.0;
     const double D = Syy / nm1 + Sxx / nm1 + (mx - my) * (mx - my) + 1e-8;
     const double dccc_dSxy = 2.0 / (D * bsd);
@@ -455,9 +458,15 @@ extern "C" int jmt_ccc_stats(int kind, int pred_dt, int64_t n, int k, const void
 
 extern "C" int jmt_ccc_finish(int kind, int world, const double* stats_all, int64_t bs, float eps,
                               float* loss, double* coef, void* stream) {
+  return jmt_ccc_finish_add(kind, world, stats_all, bs, eps, nullptr, loss, coef, stream);
+}
+
+extern "C" int jmt_ccc_finish_add(int kind, int world, const double* stats_all, int64_t bs,
+                                  float eps, const float* add, float* loss, double* coef,
+                                  void* stream) {
   JMT_CHECK_ARG(world >= 1 && stats_all && loss && coef, "jmt_ccc_finish: bad args");
   hipLaunchKernelGGL(ccc_finish_kernel, dim3(1), dim3(64), 0, as_stream(stream), kind, world,
-                     stats_all, bs, eps, loss, coef);
+                     stats_all, bs, eps, add, loss, coef);
   JMT_LAUNCH_CHECK("jmt_ccc_finish");
   return JMT_OK;
 }

@@ -158,7 +158,40 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-__device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
+// One LDS-DMA wave-instruction (global_load_lds_dwordx4: 16 B per lane from `src` to the
+// wave-uniform LDS address `lds_dst` + 16 * lane), issued from inline asm so that the compiler
+// does not track it: hipcc (ROCm 7.2) treats every pending LDS-DMA as a possible writer of any
+// ds_read_b64_tr_b16 it schedules and puts an s_waitcnt vmcnt(0) in front of the first transposed
+// read after it — draining the prefetch (the next K-tile in the GEMMs, the next K tile under the
+// P V phase of the attention forward; visible in their .s).  Every kernel that stages through
+// this waits for its DMA explicitly (vmcnt, then a barrier before the reads), and M0 is written
+// and restored inside the statement (cdna_hip_programming.md §5.7).  The ASan build compiles
+// device code at -O0, where the "s" operand cannot be proven uniform; its kernels are never
+// launched, so it takes the builtin.
+__device__ __forceinline__ void glds16_asm(const void* src, const void* lds_dst) {
+#if !defined(__OPTIMIZE__)
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+#else
+  const uint32_t a = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(a)
+      : "memory");
+#endif
+}
+
+// The same instruction from the builtin: hipcc counts it in its own s_waitcnt bookkeeping (and
+// drains it before transposed LDS reads, above).  The attention kernels load their row operands
+// (Q, dO) into registers with plain loads that hipcc waits for by counting the VMEM operations
+// issued after them; with the DMA hidden those counts come out short and every such wait
+// over-waits for the DMA in flight (attention backward +10 %, scripts/bench_attn.py), so they
+// keep the builtin.
+__device__ __forceinline__ void glds16(const void* src, const void* lds_dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }

@@ -858,7 +858,7 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
       return JMT_OK;
     }
   }
-  if (cfg == 40) cfg = 5;                    // persistent configs not applicable: same tiles
+  if (cfg == 40 || cfg == 42) cfg = 5;      // persistent configs not applicable: same tiles
   if (cfg == 41) cfg = 20;
   if (dt == JMT_F32 && cfg >= 10) cfg = 1;   // occupancy configs: 16-bit only
   if (cfg == 30 && !d->a_kmajor) cfg = 5;    // 160-row tile: K-major A only

@@ -162,32 +162,8 @@ __device__ __forceinline__ void chunk_src(int id, int& row, int& kk) {
   }
 }
 
-// One LDS-DMA wave-instruction (global_load_lds_dwordx4: 16 B per lane from `src` to the
-// wave-uniform LDS address `lds` + 16 * lane), issued from inline asm so that the compiler does
-// not track it: hipcc (ROCm 7.2) treats every pending LDS-DMA as a possible writer of any
-// ds_read_b64_tr_b16 it schedules and puts an s_waitcnt vmcnt(0) in front of the first
-// transposed read of each K-tile — draining the whole prefetch pipeline on every MN-major
-// operand (NN dgrads, TN wgrads; visible in the .s of the persistent kernel).  Every wait for
-// this DMA in the GEMM kernels is explicit (wait_vm / wait_tiles / wait_young + s_barrier), and
-// M0 is written and restored inside the statement (cdna_hip_programming.md §5.7).
-// (The ASan build compiles device code at -O0, where the "s" operand cannot be proven uniform;
-// its kernels are never launched, so it takes the builtin.)
-__device__ __forceinline__ void glds_asm(const void* src, const char* lds) {
-#if !defined(__OPTIMIZE__)
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
-#else
-  const uint32_t a = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds);
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(a)
-      : "memory");
-#endif
-}
+// One LDS-DMA wave-instruction from inline asm (common.h glds16: why hipcc must not see it).
+__device__ __forceinline__ void glds_asm(const void* src, const char* lds) { glds16_asm(src, lds); }
 
 // LDS-DMA staging of one FULL K-tile of one operand (ROWS*KB bytes = ROWS*KB/1024 wave
 // instructions spread over the block's waves).  Rows past the matrix edge are clamped to a valid

@@ -116,6 +116,7 @@ _PROTOS = {
                            c_int, c_vp]),
     "jmt_ccc_stats": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_vp, c_f, c_f, c_f, c_vp, c_vp]),
     "jmt_ccc_finish": (c_int, [c_int, c_int, c_vp, c_i64, c_f, c_vp, c_vp, c_vp]),
+    "jmt_ccc_finish_add": (c_int, [c_int, c_int, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp]),
     "jmt_ccc_bwd": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_vp, c_f, c_f, c_f, c_vp, c_vp,
                             c_vp, c_vp]),
     "jmt_mask_indices": (c_int, [c_i64, c_vp, c_f, c_vp, c_vp, c_vp]),
@@ -135,11 +136,15 @@ _PROTOS = {
     "jmt_amp_check": (c_int, [c_i64, c_vp, c_vp, c_vp]),
     "jmt_sgd_step_amp": (c_int, [c_i64, c_vp, c_vp, c_vp, c_f, c_f, c_f, c_f, c_int, c_int, c_vp,
                                  c_vp, c_int, c_vp]),
+    "jmt_sgd_step_amp_zero": (c_int, [c_i64, c_vp, c_vp, c_vp, c_f, c_f, c_f, c_f, c_int, c_int,
+                                      c_vp, c_vp, c_int, c_vp]),
     "jmt_amp_update": (c_int, [c_vp, c_f, c_f, c_int, c_vp]),
     "jmt_gather_rows": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64,
                                 c_vp]),
     "jmt_sgd_step": (c_int, [c_i64, c_vp, c_vp, c_vp, c_f, c_f, c_f, c_f, c_int, c_int, c_f,
                              c_vp, c_int, c_vp]),
+    "jmt_sgd_step_zero": (c_int, [c_i64, c_vp, c_vp, c_vp, c_f, c_f, c_f, c_f, c_int, c_int, c_f,
+                                  c_vp, c_int, c_vp]),
 }
 
 EXPORTED = tuple(_PROTOS)
@@ -165,7 +170,7 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.jmt_abi_version() != 4:
+    if lib.jmt_abi_version() != 5:
         raise JMTError("libjmt_hip.so ABI version mismatch")
     cfg = int(os.environ.get("JMT_GEMM_CFG", "0"))   # development: force a GEMM pipeline config
     dbg = int(os.environ.get("JMT_GEMM_DBG", "0"))   # development: gemm.hip ablation flags

@@ -111,9 +111,16 @@ def _grad_done(*ps) -> None:
         _grad_hook([p for p in ps if p is not None and p.requires_grad])
 
 
+# Bumped by every in-place parameter-gradient write (_grad_buffer: every HIP writer asks for its
+# buffer there): jmt.optim.FusedSGD skips its zero fill while nothing has written a gradient since
+# its last step zeroed them (jmt_sgd_step_zero).
+_grad_gen = [0]
+
+
 def _grad_buffer(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     if p is None or not p.requires_grad:
         return None
+    _grad_gen[0] += 1
     streams.join_after_backward()
     if p.grad is None:
         p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
@@ -1067,7 +1074,7 @@ class CCCLossFn(Function):
     reference computes after its DataParallel gather."""
 
     @staticmethod
-    def forward(ctx, pred, label, kind, k, ignore, lo, hi, eps, bs, group):
+    def forward(ctx, pred, label, kind, k, ignore, lo, hi, eps, bs, group, add=None):
         dev = pred.device
         pred_c = pred if pred.is_contiguous() else pred.contiguous()
         lab = label
@@ -1085,26 +1092,32 @@ class CCCLossFn(Function):
                 dist.all_gather_into_tensor(stats_all, stats, group=group)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         coef = torch.empty(8, dtype=torch.float64, device=dev)
-        ops.ccc_finish(kind, world, stats_all, bs, eps, loss, coef)
+        if add is not None and (add.dtype != torch.float32 or add.numel() != 1):
+            raise ValueError("ccc loss: `add` must be an fp32 scalar")
+        ops.ccc_finish(kind, world, stats_all, bs, eps, loss, coef, add=add)
         ctx.save_for_backward(pred_c, lab, coef)
-        ctx.meta = (kind, k, ignore, lo, hi, pred.shape)
+        ctx.meta = (kind, k, ignore, lo, hi, pred.shape, add is not None)
         return loss
 
     @staticmethod
     def backward(ctx, g):
         pred, lab, coef = ctx.saved_tensors
-        kind, k, ignore, lo, hi, shape = ctx.meta
+        kind, k, ignore, lo, hi, shape, has_add = ctx.meta
         g = g.to(torch.float32) if g.dtype != torch.float32 else g
         g = g.contiguous()
         dpred = torch.empty_like(pred)
         ops.ccc_bwd(kind, pred, lab, k, ignore, lo, hi, coef, g, dpred)
-        return dpred.view(shape), None, None, None, None, None, None, None, None, None
+        # d(add + loss) / d add = 1: the incoming gradient as is (no kernel)
+        return (dpred.view(shape), None, None, None, None, None, None, None, None, None,
+                g if has_add else None)
 
 
-def ccc_loss(pred, label, eps=1e-8, digitize_num=1, rng=(-1.0, 1.0), group=None):
+def ccc_loss(pred, label, eps=1e-8, digitize_num=1, rng=(-1.0, 1.0), group=None, add=None):
+    """add: an fp32 scalar (e.g. the other head's loss) returned summed with this loss by the
+    finish kernel — train.py:311's v_loss + a_loss without an add launch."""
     k = int(digitize_num)
     return CCCLossFn.apply(pred, label, 0, k, 0.0, float(rng[0]), float(rng[1]), float(eps), 1,
-                           group)
+                           group, add)
 
 
 def ccc_loss_ignore(pred, label, ignore=-5.0, group=None):

@@ -410,9 +410,14 @@ def ccc_stats(kind, pred, label, k, ignore, lo, hi, stats):
               lo, hi, stats.data_ptr(), stream())
 
 
-def ccc_finish(kind, world, stats_all, bs, eps, loss, coef):
-    _lib.call("jmt_ccc_finish", kind, world, stats_all.data_ptr(), bs, eps, loss.data_ptr(),
-              coef.data_ptr(), stream())
+def ccc_finish(kind, world, stats_all, bs, eps, loss, coef, add=None):
+    """add (fp32 scalar tensor or None): loss = add + this loss, in the same kernel."""
+    if add is None:
+        _lib.call("jmt_ccc_finish", kind, world, stats_all.data_ptr(), bs, eps, loss.data_ptr(),
+                  coef.data_ptr(), stream())
+    else:
+        _lib.call("jmt_ccc_finish_add", kind, world, stats_all.data_ptr(), bs, eps,
+                  add.data_ptr(), loss.data_ptr(), coef.data_ptr(), stream())
 
 
 HEAD_HID, HEAD_KMAX = 128, 24      # csrc/head.hip
@@ -481,8 +486,10 @@ def mask_indices(label: torch.Tensor, ignore: float):
 # ------------------------------------------------------------------------------------ SGD
 
 def sgd_step(param, grad, buf, lr, momentum, dampening, weight_decay, nesterov, first,
-             grad_scale=1.0, shadow=None):
-    _lib.call("jmt_sgd_step", param.numel(), param.data_ptr(), grad.data_ptr(),
+             grad_scale=1.0, shadow=None, zero_grad=False):
+    """zero_grad: grad is zeroed by the same kernel after it is read (jmt_sgd_step_zero)."""
+    _lib.call("jmt_sgd_step_zero" if zero_grad else "jmt_sgd_step", param.numel(),
+              param.data_ptr(), grad.data_ptr(),
               buf.data_ptr() if buf is not None else None, lr, momentum, dampening, weight_decay,
               int(nesterov), int(first), grad_scale,
               shadow.data_ptr() if shadow is not None else None,

@@ -20,7 +20,11 @@ from . import ops
 class FusedSGD:
     def __init__(self, params: Iterable[torch.nn.Parameter], lr: float, momentum: float = 0.0,
                  dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
-                 shadow_dtype: Optional[torch.dtype] = None):
+                 shadow_dtype: Optional[torch.dtype] = None, fuse_zero_grad: bool = False):
+        """fuse_zero_grad: the step kernel zeroes each gradient after reading it (jmt_sgd_step_zero)
+        and the next zero_grad() issues nothing while no gradient has been written since — the
+        training step of train.py:96-315 without a fill launch.  Off by default: torch's
+        optimizer.step() leaves .grad readable until zero_grad()."""
         self.params: List[torch.nn.Parameter] = list(params)
         assert self.params, "no parameters"
         dev = self.params[0].device
@@ -55,12 +59,25 @@ class FusedSGD:
             F.register_shadow(p, self.shadow[off:off + p.numel()].view_as(p)
                               if self.shadow is not None else None)
         self.first = True
+        self.fuse_zero_grad = bool(fuse_zero_grad)
+        # the gradients are known to be zero while nothing has written one since the last fill /
+        # zeroing step (functional._grad_gen counts the HIP writers; torch autograd accumulation
+        # into .grad is caught by the post-accumulate hooks)
+        self._clean_gen = F._grad_gen[0]
+        for p in self.params:
+            p.register_post_accumulate_grad_hook(lambda _p: F._grad_gen.__setitem__(
+                0, F._grad_gen[0] + 1))
 
     def zero_grad(self, set_to_none: bool = False):
-        self.flat_g.zero_()
+        """optimizer.zero_grad().  With fuse_zero_grad the step kernel already zeroed the
+        gradients, so after a step (and no gradient write since) this issues nothing."""
         for p, g in zip(self.params, self._gviews):
             if p.grad is None or p.grad.data_ptr() != g.data_ptr():
                 p.grad = g
+                self._clean_gen = None
+        if not self.fuse_zero_grad or self._clean_gen != F._grad_gen[0]:
+            self.flat_g.zero_()
+            self._clean_gen = F._grad_gen[0]
 
     @torch.no_grad()
     def step_amp(self, amp_state: torch.Tensor):
@@ -68,12 +85,13 @@ class FusedSGD:
         the momentum buffer is initialised is then decided on the device (steps_taken), so plain
         step() calls cannot follow scaled ones."""
         self._amp = True
-        _lib.call("jmt_sgd_step_amp", self.numel, self.flat_p.data_ptr(), self.flat_g.data_ptr(),
+        _lib.call("jmt_sgd_step_amp_zero" if self.fuse_zero_grad else "jmt_sgd_step_amp", self.numel, self.flat_p.data_ptr(), self.flat_g.data_ptr(),
                   self.buf.data_ptr() if self.buf is not None else None, self.lr, self.momentum,
                   self.dampening, self.weight_decay, int(self.nesterov), int(self.first),
                   amp_state.data_ptr(),
                   self.shadow.data_ptr() if self.shadow is not None else None,
                   ops.dt(self.shadow) if self.shadow is not None else 1, ops.stream())
+        self._clean_gen = F._grad_gen[0]
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0):
@@ -81,8 +99,10 @@ class FusedSGD:
             raise RuntimeError("FusedSGD: step() after GradScaler steps (first-step state is on "
                                "the device); keep using scaler.step(opt)")
         ops.sgd_step(self.flat_p, self.flat_g, self.buf, self.lr, self.momentum, self.dampening,
-                     self.weight_decay, self.nesterov, self.first, grad_scale, self.shadow)
+                     self.weight_decay, self.nesterov, self.first, grad_scale, self.shadow,
+                     zero_grad=self.fuse_zero_grad)
         self.first = False
+        self._clean_gen = F._grad_gen[0]
 
 
 class GradScaler:

@@ -27,6 +27,12 @@ class CCCLoss(nn.Module):
         return F.ccc_loss(x, y, eps=self.eps, digitize_num=self.digitize_num, rng=self.range,
                           group=jdist.loss_group())
 
+    def forward_add(self, x, y, prev):
+        """prev + self(x, y) with the sum formed by the loss's own finish kernel (train.py:311's
+        `v_loss + a_loss` as one expression: same value, one fp32 rounding, no add launch)."""
+        return F.ccc_loss(x, y, eps=self.eps, digitize_num=self.digitize_num, rng=self.range,
+                          group=jdist.loss_group(), add=prev)
+
 
 class CELoss(nn.Module):
     """loss.py:34-51: cross entropy against labels digitized into `digitize_num` bins

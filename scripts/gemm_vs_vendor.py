@@ -37,23 +37,28 @@ SHAPES = [
 ]
 
 
-def make(layout, b, M, N, K, dev):
+def make(layout, b, M, N, K, dev, pad=0):
+    """pad: extra elements on every operand row (row strides off the power of two)."""
     g = torch.Generator(device=dev).manual_seed(1)
-    r = lambda *s: (torch.rand(*s, device=dev, generator=g) * 2 - 1).bfloat16()
+    r = lambda rows, cols: (torch.rand(b, rows, cols + pad, device=dev, generator=g) * 2 - 1
+                            ).bfloat16()[:, :, :cols]
     if layout == "NT":
-        a, w = r(b, M, K), r(b, N, K)
+        a, w = r(M, K), r(N, K)
         ref = lambda: torch.bmm(a, w.transpose(1, 2))
-        kw = dict(a_kmajor=True, b_kmajor=True, lda=K, ldb=K, sA=(M * K, 0), sB=(N * K, 0))
+        kw = dict(a_kmajor=True, b_kmajor=True, lda=K + pad, ldb=K + pad,
+                  sA=(M * (K + pad), 0), sB=(N * (K + pad), 0))
         cdt = BF16
     elif layout == "NN":
-        a, w = r(b, M, K), r(b, K, N)
+        a, w = r(M, K), r(K, N)
         ref = lambda: torch.bmm(a, w)
-        kw = dict(a_kmajor=True, b_kmajor=False, lda=K, ldb=N, sA=(M * K, 0), sB=(N * K, 0))
+        kw = dict(a_kmajor=True, b_kmajor=False, lda=K + pad, ldb=N + pad,
+                  sA=(M * (K + pad), 0), sB=(K * (N + pad), 0))
         cdt = BF16
     else:
-        a, w = r(b, K, M), r(b, K, N)
+        a, w = r(K, M), r(K, N)
         ref = lambda: torch.bmm(a.transpose(1, 2), w)     # (vendor writes bf16, ours fp32)
-        kw = dict(a_kmajor=False, b_kmajor=False, lda=M, ldb=N, sA=(M * K, 0), sB=(N * K, 0))
+        kw = dict(a_kmajor=False, b_kmajor=False, lda=M + pad, ldb=N + pad,
+                  sA=(K * (M + pad), 0), sB=(K * (N + pad), 0))
         cdt = F32
     c = torch.empty(b, M, N, device=dev, dtype=torch.float32 if cdt == F32 else torch.bfloat16)
     kw.update(M=M, N=N, K=K, ab_dtype=BF16, c_dtype=cdt, a=[a.data_ptr()], b=[w.data_ptr()],
@@ -78,15 +83,18 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--cfg", type=int, nargs="*", default=[0])
     ap.add_argument("--no-vendor", action="store_true")
+    ap.add_argument("--pad", type=int, nargs="*", default=[0],
+                    help="operand row padding (elements) per pass")
     ap.add_argument("--dbg", type=int, nargs="*", default=[0],
                     help="ablation flags per arm (1 skip MFMA, 2 skip epilogue, 32 drain stores)")
     args = ap.parse_args()
     lib = _lib.load()
     dev = "cuda"
-    for name, layout, b, M, N, K in SHAPES:
+    for name, layout, b, M, N, K, pad in [s + (pd,) for s in SHAPES for pd in args.pad]:
         if args.only and not any(s in name for s in args.only.split(",")):
             continue
-        a, w, c, ref, kw = make(layout, b, M, N, K, dev)
+        a, w, c, ref, kw = make(layout, b, M, N, K, dev, pad)
+        name = name + (f" pad{pad}" if pad else "")
         arms = {}
         if not args.no_vendor:
             arms["vendor"] = ref

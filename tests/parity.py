@@ -155,7 +155,7 @@ def ref_taps(c: dict) -> dict:
     reference goldens' 8 sampled rows to 1e-4 (tests/test_oracle.py); the strict suite compares
     every row, because 16-bit errors of an intermediate gradient concentrate in the few rows
     where a ReLU mask flips (chaotic: different rows for different roundings), so an 8-row
-    sample is hit-or-miss (scripts/r03/sa_probe2.py)."""
+    sample is hit-or-miss."""
     if c["tag"] not in _REF_TAPS:
         from tests.oracle_cases import oracle_tt
         torch.set_num_threads(min(16, max(1, len(os.sched_getaffinity(0)))))
@@ -312,3 +312,128 @@ def check_vs_ref16(golden: dict, c: dict, gpu: dict, emu: dict, cd) -> list:
     if not np.isfinite(g["pgrad_max"]):
         bad.append(("pgrad_max", g["pgrad_max"], "finite"))
     return bad
+
+
+def window_subset_check(cd=torch.bfloat16, B: int = 64, T: int = 300, win=(0, 21, 42, 63),
+                        perturb: float = 0.0, model_builder=None) -> dict:
+    """configs[2] at the bench shape in the compute dtype with the conditioned hash-init weights
+    (oracle/hashinit.py GAINS_COND_T300): the GPU runs the WHOLE batch; the objective weights
+    (hashinit.proj_weights) are zero outside the windows `win`, so every gradient is exactly those
+    windows' (attention runs within a window in TRANSFORMER mode) and the fp32 oracle on them is
+    the reference.  Every prediction of those windows (relative to the largest) and EVERY
+    parameter gradient (relative L2) must sit within the strict 16-bit bound of this module:
+    min(CEIL, K_STRICT x max(the rounding-emulating oracle's error, 2u)).  The full-batch CCC
+    losses of the GPU predictions are checked against the oracle's CCC of the same predictions.
+    `perturb` scales the GPU model's cross_attention_v.out_proj.weight by (1 + perturb) AFTER the
+    oracle's weights are taken (the check must then fail: bench.py --parity-perturb).
+    Used by tests/test_gpu_configs.py and bench.py's `parity` field."""
+    import contextlib
+    from losses.loss import CCCLoss
+    from oracle import jmt_ref as R
+    from oracle.hashinit import GAINS_COND_T300, features, labels, proj_weights
+    win = list(win)
+    c = dict(tag="c3b", jm="TRANSFORMER", fmt="FC", H=1, L=1, B=B, T=T, vin=2048,
+             gains=GAINS_COND_T300)
+    m, fc = build_tt(c) if model_builder is None else model_builder(c)
+    audio = torch.from_numpy(features("c3b.audio", (B, T, 1024)))
+    video = torch.from_numpy(features("c3b.video", (B, T, 2048)))
+    lv = torch.from_numpy(labels("c3b.lv", (B, T)))
+    la = torch.from_numpy(labels("c3b.la", (B, T)))
+    wsub = [torch.from_numpy(proj_weights(f"c3b.w{k}", (T, len(win)))) for k in "va"]
+    wfull = [torch.zeros(T, B) for _ in range(2)]
+    for wf, ws in zip(wfull, wsub):
+        wf[:, win] = ws
+    n = float(T * len(win))
+    p0 = {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
+    fp0 = {k: v.detach().float().cpu() for k, v in fc.state_dict().items()}
+    if perturb:
+        with torch.no_grad():
+            m.mm_transformer.cross_attention_v.out_proj.weight.mul_(1.0 + perturb)
+    crit = CCCLoss(1)
+    store = {}
+    taps.enable(store)                 # encoder / cross-attention outputs (jmt/taps.py)
+    try:
+        with JF.compute_mode(cd):
+            vo, ao = m(fc(audio.to(DEV)), video.to(DEV))          # (T, B) seq-first
+            obj = (vo.float() * wfull[0].to(DEV)).sum() / n + \
+                (ao.float() * wfull[1].to(DEV)).sum() / n
+            obj.backward()
+            with torch.no_grad():
+                l1 = crit(vo.reshape(1, -1), lv.to(DEV).view(1, -1))
+                l2 = crit(ao.reshape(1, -1), la.to(DEV).view(1, -1))
+    finally:
+        taps.disable()
+    torch.cuda.synchronize()
+    gtaps = {k: v["val"][win].float().cpu() for k, v in store.items()
+             if k.startswith(("enc.", "ca."))}
+    del store
+    gpu = {k: p.grad.detach().float().cpu() for k, p in m.named_parameters() if p.grad is not None}
+    gpu.update({"fc." + k: p.grad.detach().float().cpu() for k, p in fc.named_parameters()})
+    rl1 = float(R.ccc_loss(vo.detach().float().cpu().reshape(1, -1), lv.reshape(1, -1)))
+    rl2 = float(R.ccc_loss(ao.detach().float().cpu().reshape(1, -1), la.reshape(1, -1)))
+    loss_err = max(abs(float(l1) - rl1), abs(float(l2) - rl2))
+
+    def oracle(emulate):
+        pp = {k: t.clone().requires_grad_(True) for k, t in p0.items()}
+        fpp = {k: t.clone().requires_grad_(True) for k, t in fp0.items()}
+        tp = {}
+        with (R.emulate_storage(emulate) if emulate else contextlib.nullcontext()):
+            aud = R.linear(audio[win], fpp["fc_layer.weight"], fpp["fc_layer.bias"])
+            rvo, rao = R.two_transformers_forward(aud, video[win], pp, 1, 1, "TRANSFORMER", "FC",
+                                                  2048, taps=tp)
+            ((rvo * wsub[0]).sum() / n + (rao * wsub[1]).sum() / n).backward()
+        g = {k: t.grad for k, t in pp.items() if t.grad is not None}
+        g.update({"fc." + k: t.grad for k, t in fpp.items()})
+        tv = {k: (t.permute(1, 0, 2) if sf else t).detach().float() for k, (t, sf) in tp.items()
+              if k.startswith(("enc.", "ca."))}
+        return rvo.detach(), rao.detach(), g, tv
+
+    rvo, rao, rg, rt = oracle(None)
+    evo, eao, eg, et = oracle(cd)
+    u = UNIT[cd]
+
+    def bound(kind, e_emu):
+        return min(CEIL[cd][kind], K_STRICT * max(e_emu, 2 * u))
+
+    def rel(a, b):
+        a, b = a.double().reshape(-1), b.double().reshape(-1)
+        return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+    rows = []
+    mx = float(max(rvo.abs().max(), rao.abs().max()))
+    for name, got, emu, ref in (("vouts", vo.detach().float().cpu()[:, win], evo, rvo),
+                                ("aouts", ao.detach().float().cpu()[:, win], eao, rao)):
+        e_gpu = float((got - ref).abs().max()) / mx
+        e_emu = float((emu - ref).abs().max()) / mx
+        rows.append((name, e_gpu, bound("out", e_emu)))
+    for k in rg:
+        rows.append((k, rel(gpu[k], rg[k]) if k in gpu else float("inf"),
+                     bound("param", rel(eg[k], rg[k]))))
+    # the encoder and cross-attention outputs of the checked windows (relative L2 per tensor;
+    # floor u/2: one rounding of the stored value): a 2 % error in one cross-attention's weights
+    # is diluted below the bf16 floor in the predictions but not in its own output
+    for k in sorted(rt):
+        e_emu = rel(et[k], rt[k])
+        rows.append((k, rel(gtaps[k], rt[k]) if k in gtaps else float("inf"),
+                     min(CEIL[cd]["inter"], K_STRICT * max(e_emu, u / 2))))
+    unused_nonzero = [k for k in gpu if k not in rg and float(gpu[k].abs().max()) != 0.0]
+    bad = [r for r in rows if not r[1] <= r[2]]
+    margin = min(r[2] / max(r[1], 1e-30) for r in rows)
+    pred = [r for r in rows if r[0] in ("vouts", "aouts")]
+    ol1 = [r for r in rows if r[0] == "mm_transformer.out_layer1.weight"]
+    spread = float(torch.cat([rvo.reshape(-1), rao.reshape(-1)]).std())
+    pred_abs = max(float((vo.detach().float().cpu()[:, win] - rvo).abs().max()),
+                   float((ao.detach().float().cpu()[:, win] - rao).abs().max()))
+    return {"pass": not bad and not unused_nonzero and loss_err <= 1e-5,
+            "quantities": len(rows), "violations": len(bad),
+            "intermediates_checked": sorted(rt),
+            "worst": [(k, round(e, 5), round(b, 5)) for k, e, b in
+                      sorted(rows, key=lambda r: -r[1] / max(r[2], 1e-30))[:3]],
+            "min_margin": round(margin, 3),
+            "pred_err_max_rel_to_largest": round(max(r[1] for r in pred), 5),
+            "pred_bound": round(min(r[2] for r in pred), 5),
+            "pred_abs_err_rel_to_spread": round(pred_abs / spread, 5),
+            "out_layer1_grad_rel_err": round(ol1[0][1], 5) if ol1 else None,
+            "out_layer1_grad_bound": round(ol1[0][2], 5) if ol1 else None,
+            "loss_abs_err_vs_oracle_ccc": float(f"{loss_err:.3g}"),
+            "unused_params_nonzero_grad": unused_nonzero}

@@ -195,7 +195,7 @@ def test_gemm_kconcat_and_pointer_tables(dt):
     assert (dW - ref).abs().max().item() <= _tol(dt, M) * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("cfg", [40, 41])
+@pytest.mark.parametrize("cfg", [40, 41, 42])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 def test_gemm_persistent(cfg, ak, bk):
     """gemm_persist_kernel (csrc/gemm_persist.hip: one block per CU walks whole 256x256 tiles
