@@ -149,7 +149,7 @@ int jmt_layernorm_bwd_dsum(int dt_in, int dt_dy, int dt_dx, int64_t rows, int D,
  * x + g*sx (r + g*sr; y or dx + g*sy / sdx; dy + g*sdy; elements), its statistics at
  * mean / rstd + g*rows, its parameters / gradients from the pointer tables (host arrays of G
  * device pointers).  Backward: dsum may be NULL (no column sums of dx); partials:
- * G * (dsum ? 3 : 2) * D * jmt_layernorm_bwd_blocks(rows) floats, 16-B aligned.  D in
+ * G * (dsum ? 3 : 2) * D * jmt_layernorm_bwd_grouped_blocks(rows) floats, 16-B aligned.  D in
  * {512, 768, 1024} with 4-element aligned rows and strides; otherwise JMT_ERR_UNSUPPORTED. */
 int jmt_layernorm_fwd_grouped(int dt_in, int dt_out, int G, int64_t rows, int D, const void* x,
                               int64_t ldx, int64_t sx, const void* r, int64_t ldr, int64_t sr,
@@ -163,6 +163,9 @@ int jmt_layernorm_bwd_grouped(int dt_in, int dt_dy, int dt_dx, int G, int64_t ro
                               void* dx, int64_t lddx, int64_t sdx, float* const* dgamma,
                               float* const* dbeta, float* const* dsum, int beta_acc,
                               float* partials, void* stream);
+/* ABI 5: the partials of jmt_layernorm_bwd_grouped hold G * (dsum ? 3 : 2) * D *
+ * jmt_layernorm_bwd_grouped_blocks(rows) floats (the grouped kernel's rows per block). */
+int jmt_layernorm_bwd_grouped_blocks(int64_t rows);
 
 /* Attention softmax (F.multi_head_attention_forward): rows of length n of the
  * fp32 score matrix S (ld) -> P = softmax(scale * S) stored as p_dt at ldp; columns [n, ldp)

@@ -56,7 +56,10 @@ __device__ __forceinline__ PItem pitem(const GemmParams& p, int w, int W) {
   return it;
 }
 
-template <typename T, class C>
+// EPI: 0 plain, 1 beta * C, 2 ReLU mask (aux), 3 both — compile-time, so that every load the
+// epilogue issues is consumed on every path (a conditional load left hipcc unsure at the loop
+// head and it waited vmcnt(4) there, draining the next K-tile's DMA every iteration)
+template <typename T, class C, int EPI>
 __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PItem& it,
                                                  f32x4 (&acc)[C::TM][C::TN],
                                                  const float* bias_lds, int lane, int wm, int wn) {
@@ -101,12 +104,32 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
 #pragma unroll
       for (int e = 0; e < 4; ++e) bias4[j][e] = 0.f;
   }
-  const float alpha = p.alpha;
+  const float alpha = p.alpha, beta = p.beta;
   const bool relu = p.relu != 0;
+  const T* auxp = (const T*)p.aux;
+  // beta * C and the ReLU-backward mask (aux > 0) of the one-block-per-tile epilogue, in its
+  // order (+ beta C, ReLU, mask); their 8-B loads of row i + 1 are in flight while row i is
+  // converted and stored.  hipcc waits for them by its own count (only its own loads and stores
+  // follow them); the DMA it cannot see is older, issued a K-tile earlier.
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 cr[2][C::TN], ar[2][C::TN];
+  constexpr bool ldc_ = (EPI & 1) != 0, lda_ = (EPI & 2) != 0;
+  auto load_row = [&](int i, u32x2 (&c)[C::TN], u32x2 (&a)[C::TN]) {
+    const int m = it.m0 + wm * C::WTM + 16 * i + rl;
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) {
+      const int n = it.n0 + wn * C::WTN + 16 * j + 4 * g;
+      if constexpr (ldc_) c[j] = *(const u32x2*)(cp + cbase + (int64_t)m * p.ldc + n);
+      if constexpr (lda_) a[j] = *(const u32x2*)(auxp + cbase + (int64_t)m * p.ldaux + n);
+    }
+  };
+  if constexpr (ldc_ || lda_) load_row(0, cr[0], ar[0]);
 #pragma unroll
   for (int i = 0; i < C::TM; ++i) {
     const int m = it.m0 + wm * C::WTM + 16 * i + rl;
     const int64_t rowo = cbase + (int64_t)m * p.ldc;
+    if constexpr (ldc_ || lda_)
+      if (i + 1 < C::TM) load_row(i + 1, cr[(i + 1) & 1], ar[(i + 1) & 1]);
 #pragma unroll
     for (int jp = 0; jp < C::TN / 2; ++jp) {
       uint32_t pk[2][2];
@@ -115,9 +138,20 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
         const int j = 2 * jp + h;
         float x[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          x[e] = acc[i][j][e] * alpha + bias4[j][e];
-          if (relu) x[e] = fmaxf(x[e], 0.f);
+        for (int e = 0; e < 4; ++e) x[e] = acc[i][j][e] * alpha + bias4[j][e];
+        if constexpr (ldc_ || lda_) {
+          const T* cv = (const T*)&cr[i & 1][j];
+          const T* av = (const T*)&ar[i & 1][j];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if constexpr (ldc_) x[e] += beta * to_f(cv[e]);
+            if (relu) x[e] = fmaxf(x[e], 0.f);
+            if constexpr (lda_)
+              if (!(to_f(av[e]) > 0.f)) x[e] = 0.f;
+          }
+        } else if (relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = fmaxf(x[e], 0.f);
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -136,7 +170,7 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
   }
 }
 
-template <typename T, bool AK, bool BK, class C>
+template <typename T, bool AK, bool BK, class C, int EPI>
 __global__ __launch_bounds__(C::NT, C::OCC)
 void gemm_persist_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -262,7 +296,7 @@ void gemm_persist_kernel(GemmParams p) {
     }
     if (go) advance_issue();
     if (++cur_kt == nkt) {                             // item done: stores behind the prefetch
-      if (!(p.dbg & 2)) persist_epilogue<T, C>(p, cur, acc, bias_lds, lane, wm, wn);
+      if (!(p.dbg & 2)) persist_epilogue<T, C, EPI>(p, cur, acc, bias_lds, lane, wm, wn);
 #pragma unroll
       for (int i = 0; i < C::TM; ++i)
 #pragma unroll
@@ -281,7 +315,7 @@ void gemm_persist_kernel(GemmParams p) {
 // LDS = 3 A images + 2 B images of 32 KiB = the whole 160 KiB, so the bias comes from scalar
 // loads.  Per iteration s: DMA A(s + 2), B(s + 1) -> wait for B(s) (issued after A(s + 1), so
 // A(s) is older and landed with it) -> barrier -> MFMAs -> barrier -> epilogue at a tile's end.
-template <typename T, bool AK, bool BK, class C>
+template <typename T, bool AK, bool BK, class C, int EPI>
 __global__ __launch_bounds__(C::NT, C::OCC)
 void gemm_persist3_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -382,7 +416,7 @@ void gemm_persist3_kernel(GemmParams p) {
       compute_tile<T, AK, BK, C>(imgA0 + (s % 3) * IA, imgB0 + (s & 1) * IB, wm, wn, acc);
     __builtin_amdgcn_s_barrier();
     if (++cur_kt == nkt) {
-      if (!(p.dbg & 2)) persist_epilogue<T, C>(p, cur, acc, nullptr, lane, wm, wn);
+      if (!(p.dbg & 2)) persist_epilogue<T, C, EPI>(p, cur, acc, nullptr, lane, wm, wn);
 #pragma unroll
       for (int i = 0; i < C::TM; ++i)
 #pragma unroll
@@ -412,11 +446,11 @@ static int num_cus() {
   return cache[dev];
 }
 
-template <typename T, bool AK, bool BK, class C, bool A3>
-static void launch_persist_cfg(const GemmParams& p, int blocks, hipStream_t st) {
+template <typename T, bool AK, bool BK, class C, bool A3, int EPI>
+static void launch_persist_epi(const GemmParams& p, int blocks, hipStream_t st) {
   void (*fn)(GemmParams);
-  if constexpr (A3) fn = gemm_persist3_kernel<T, AK, BK, C>;
-  else fn = gemm_persist_kernel<T, AK, BK, C>;
+  if constexpr (A3) fn = gemm_persist3_kernel<T, AK, BK, C, EPI>;
+  else fn = gemm_persist_kernel<T, AK, BK, C, EPI>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -428,6 +462,17 @@ static void launch_persist_cfg(const GemmParams& p, int blocks, hipStream_t st) 
   const size_t lds = A3 ? (size_t)3 * C::BM * C::KB + (size_t)2 * C::BN * C::KB
                        : (size_t)C::S * C::STAGE + (size_t)nb * sizeof(float);
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(C::NT), lds, st, p);
+}
+
+template <typename T, bool AK, bool BK, class C, bool A3>
+static void launch_persist_cfg(const GemmParams& p, int blocks, hipStream_t st) {
+  const int epi = (p.beta != 0.f ? 1 : 0) | (p.aux != nullptr ? 2 : 0);
+  switch (epi) {
+    case 0: launch_persist_epi<T, AK, BK, C, A3, 0>(p, blocks, st); break;
+    case 1: launch_persist_epi<T, AK, BK, C, A3, 1>(p, blocks, st); break;
+    case 2: launch_persist_epi<T, AK, BK, C, A3, 2>(p, blocks, st); break;
+    default: launch_persist_epi<T, AK, BK, C, A3, 3>(p, blocks, st); break;
+  }
 }
 
 template <typename T, class C, bool A3 = false>
@@ -464,10 +509,10 @@ int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int 
   const int dt = d->ab_dtype;
   const int batch0 = d->batch0 < 1 ? 1 : d->batch0;
   const long nbias = p.bias_mode == 1 ? (long)(d->n_bias > 0 ? batch0 : 1) * d->N : 0;
-  const bool ok = dt != JMT_F32 && d->c_dtype == dt && splits == 1 && d->beta == 0.f &&
-                  d->aux == nullptr && d->n_dbias == 0 && d->M % 256 == 0 && d->N % 256 == 0 &&
-                  d->K % 64 == 0 && d->K >= 128 && p.c_vec8 && p.bias_mode != 2 &&
-                  nbias <= kPersistBias;
+  // (beta * C / the ReLU mask: 8-B loads of C / aux rows in the epilogue — c_vec4 covers aux)
+  const bool ok = dt != JMT_F32 && d->c_dtype == dt && splits == 1 && d->n_dbias == 0 &&
+                  d->M % 256 == 0 && d->N % 256 == 0 && d->K % 64 == 0 && d->K >= 128 &&
+                  p.c_vec8 && p.c_vec4 && p.bias_mode != 2 && nbias <= kPersistBias;
   if (!ok) return 0;
   if (forced >= 40 && forced <= 42) return forced;
   if (forced != 0 || env == 0) return 0;

@@ -844,6 +844,10 @@ extern "C" int jmt_layernorm_bwd_blocks(int64_t rows) {
   return (int)((rows + LN_ROWS_PER_BLOCK - 1) / LN_ROWS_PER_BLOCK);
 }
 
+extern "C" int jmt_layernorm_bwd_grouped_blocks(int64_t rows) {
+  return (int)((rows + LN_ROWS_PER_BLOCK_GROUPED - 1) / LN_ROWS_PER_BLOCK_GROUPED);
+}
+
 extern "C" int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, int D,
                                  const void* x, int64_t ldx, const void* r, int64_t ldr,
                                  const void* dy, int64_t lddy, const float* mean,
@@ -1121,7 +1125,7 @@ extern "C" int jmt_layernorm_bwd_grouped(int dt_in, int dt_dy, int dt_dx, int G,
     t2.p[g] = dsum ? dsum[g] : nullptr;
   }
   hipStream_t st = as_stream(stream);
-  const int nblk = (int)((rows + LN_ROWS_PER_BLOCK_GROUPED - 1) / LN_ROWS_PER_BLOCK_GROUPED);
+  const int nblk = jmt_layernorm_bwd_grouped_blocks(rows);
   const dim3 grid((unsigned)nblk, (unsigned)G);
   // development A/B: rows in flight per wave (JMT_LN_BWD_U=4; D = 512, one dtype throughout)
   static const int ln_u = [] {

@@ -109,6 +109,7 @@ _PROTOS = {
                                    c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                    c_i64, c_f, c_vp]),
     "jmt_colsum_blocks": (c_int, [c_i64]),
+    "jmt_layernorm_bwd_grouped_blocks": (c_int, [c_i64]),
     "jmt_colsum": (c_int, [c_int, c_i64, c_int, c_vp, c_i64, c_vp, c_int, c_vp, c_vp]),
     "jmt_colsum_grouped": (c_int, [c_int, c_int, c_i64, c_int, c_vp, c_i64, c_i64, c_vp, c_int,
                                    c_vp, c_vp]),

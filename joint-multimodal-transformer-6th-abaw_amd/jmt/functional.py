@@ -881,13 +881,14 @@ def attn_backward(saved, go, dq, dk, dv):
     if fused in ("small", "short"):
         # the kernel's layout contract covers the gradient buffers too: a misaligned one is
         # written through an aligned (contiguous) temporary and copied back.  Aliased buffers
-        # (packed qkv) share one temporary.
+        # (packed qkv — possibly distinct view objects of one buffer) share one temporary: keyed
+        # on the memory the view spans, not on the Python object.
         outs, tmps = [], {}
         for buf, col in ((dq, qcol), (dk, kcol), (dv, vcol)):
             if _small_aligned(buf, col, cd):
                 outs.append((buf, col))
                 continue
-            key = id(buf)
+            key = (buf.data_ptr(), tuple(buf.shape), tuple(buf.stride()))
             if key not in tmps:
                 tmps[key] = (buf, buf.clone(memory_format=torch.contiguous_format))
             outs.append((tmps[key][1], col))
@@ -1128,6 +1129,9 @@ def ccc_loss_ignore(pred, label, ignore=-5.0, group=None):
     return CCCLossFn.apply(pred, label, 1, 1, float(ignore), -1.0, 1.0, 0.0, int(bs), group)
 
 
+_CE_EDGES: dict = {}
+
+
 class CELossFn(Function):
     """losses/loss.py:34-51 CELoss on the device: digitize + weighted log-softmax NLL in one
     statistics kernel, (optional) all-gather of 4 doubles per rank, one finish kernel; backward
@@ -1138,7 +1142,22 @@ class CELossFn(Function):
         dev = x.device
         xc = x if x.is_contiguous() else x.contiguous()
         lab = label.reshape(-1)
-        if lab.dtype != torch.float32 or not lab.is_contiguous():
+        if lab.dtype == torch.float64:
+            # the reference digitizes the label's own values against float64 edges
+            # (loss.py:48, np.digitize): a float64 label within fp32 rounding of an edge must
+            # not change bin by the cast, so the bin is found here in float64 and the kernel
+            # gets an fp32 representative of it (the bin centre; lo - 1 below the range, where
+            # the reference raises and the kernel yields NaN)
+            key = (lo, hi, k, str(dev))
+            edges = _CE_EDGES.get(key)
+            if edges is None:            # numpy's linspace bit for bit (torch's differs by ulps)
+                import numpy as np
+                edges = _CE_EDGES[key] = torch.from_numpy(np.linspace(lo, hi, num=k + 1)).to(dev)
+            idx = torch.bucketize(lab, edges, right=True) - 1           # np.digitize - 1
+            centre = ((edges[:-1] + edges[1:]) * 0.5).float()
+            lab = torch.where(idx < 0, torch.full_like(centre[:1], lo - 1.0),
+                              centre[idx.clamp(0, k - 1)]).contiguous()
+        elif lab.dtype != torch.float32 or not lab.is_contiguous():
             lab = ops.cast(lab, torch.float32)
         w = None
         if weights is not None:

@@ -207,7 +207,7 @@ def layernorm_bwd_grouped(X, R, dY, mean, rstd, gammas, dX, dgammas, dbetas, dsu
     alive until the launches are ordered) or None when the shape is not covered."""
     G, D = X.shape[0], X.shape[-1]
     rows = X[0].numel() // D
-    nblk = _lib.load().jmt_layernorm_bwd_blocks(rows)
+    nblk = _lib.load().jmt_layernorm_bwd_grouped_blocks(rows)
     ns = 3 if dsums is not None else 2
     part = torch.empty(max(nblk, 1) * ns * D * G, dtype=torch.float32, device=X.device)
     rc = _lib.load().jmt_layernorm_bwd_grouped(

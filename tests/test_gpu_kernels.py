@@ -237,6 +237,35 @@ def test_gemm_persistent(cfg, ak, bk):
             ref = torch.relu(0.75 * (Al[i] @ Bl[i]) + bias[i])
             err = (C2[i].float() - ref).abs().max().item()
             assert err <= 1e-2 * ref.abs().max().item(), (cfg, M, N, K, i, err)
+    # beta * C and the ReLU-backward mask (aux > 0) epilogue forms (the stacked-stream / FFN
+    # dgrads): C accumulates, the mask zeroes
+    M, N, K, nb = 4608, 512, 256, 3
+    A, Al, lda, sa = _operand(M, K, ak, BF16, batch=nb, gen=g)
+    Bs, Bl_t, ldb, sb = _operand(N, K, bk, BF16, batch=nb, gen=g)
+    Bl = Bl_t.transpose(1, 2)
+    C0 = torch.randn(nb, M, N, device=DEV, generator=g).to(bf)
+    aux = torch.randn(nb, M, N, device=DEV, generator=g).to(bf)
+    for beta, use_aux in ((1.0, False), (0.0, True), (0.5, True)):
+        C = C0.clone()
+        outs = []                    # (beta accumulates: each execution starts from C0)
+        for dbg in (0, 32):
+            C.copy_(C0)
+            lib.jmt_gemm_set_debug((cfg << 8) | dbg)
+            try:
+                ops.gemm(M=M, N=N, K=K, ab_dtype=BF16, c_dtype=BF16, a=[A.data_ptr()], lda=lda,
+                         a_kmajor=ak, sA=(sa, 0), b=[Bs.data_ptr()], ldb=ldb, b_kmajor=bk,
+                         sB=(sb, 0), c=[C.data_ptr()], ldc=N, sC=(M * N, 0), batch0=nb,
+                         beta=beta, aux=aux if use_aux else None, ldaux=N, splits=1, device=DEV)
+            finally:
+                lib.jmt_gemm_set_debug(0)
+            outs.append(C.clone())
+        assert torch.equal(outs[0], outs[1])
+        for i in range(nb):
+            ref = Al[i] @ Bl[i] + beta * C0[i].float()
+            if use_aux:
+                ref = torch.where(aux[i].float() > 0, ref, torch.zeros_like(ref))
+            err = (outs[0][i].float() - ref).abs().max().item()
+            assert err <= 1e-2 * ref.abs().max().item(), (cfg, beta, use_aux, i, err)
     if ak:
         # K-concat A (4 segments of 128) x (K-major | MN-major) B into a C pointer table of two
         # (batch1-strided) outputs, one bias for every batch entry
