@@ -214,6 +214,17 @@ int jmt_attn_bwd_km(int dt, int N, int H, int Lq, int Lk, int dh, const void* go
                     void* ds_out, int64_t ldt, void* dq, int64_t sdq_l, int64_t sdq_n,
                     float scale, void* stream);
 
+/* Key-side attention gradients from the handed-over probabilities (round 4): per (n, h)
+ * dV = P^T dO and dK = dS^T Q, P / dS as jmt_attn_bwd writes them (row (n*H + h)*Lq + q, keys in
+ * columns, row stride ldp >= 64 ceil(Lk / 64): the kernel reads whole 64-key tiles; columns past
+ * Lk only feed outputs that are not stored).  dO / Q / dK / dV seq-first views as jmt_attn_bwd's
+ * operands (row stride s*_l, batch stride s*_n, head h at columns 512 h).  16-bit, dh = 512.
+ * Replaces the two batched TN jmt_gemm calls (M = Lk, N = dh, K = Lq) of the same products. */
+int jmt_attn_dkdv(int dt, int N, int H, int Lq, int Lk, int dh, const void* p, const void* ds,
+                  int64_t ldp, const void* go, int64_t sgo_l, int64_t sgo_n, const void* q,
+                  int64_t sq_l, int64_t sq_n, void* dk, int64_t sdk_l, int64_t sdk_n, void* dv,
+                  int64_t sdv_l, int64_t sdv_n, void* stream);
+
 /* Fused attention over short sequences, the whole backward in one kernel (Lq, Lk <= 32, 16-bit,
  * dh = 512; the batch-axis self-attention of mm_transformers.py:119-146 at B = 32 and every
  * attention of the T = 16 real-data configuration): same element addressing as jmt_attn_*,

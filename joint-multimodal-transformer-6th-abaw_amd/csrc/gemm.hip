@@ -466,7 +466,141 @@ void gemm_kernel(GemmParams p) {
   trace_stamp(p, 2);
   gemm_epilogue<T, O, C>(p, cur, acc, lane, wm, wn);
   if constexpr (RS) rowsum_store<C>(p, cur, rsum, lane, wm);
+  if (p.splits > 1 && p.counters) {
+    if (p.c_dtype == JMT_F32) splitk_fixup<float, C>(p, cur);
+    else splitk_fixup<T, C>(p, cur);
+  }
   trace_stamp(p, 3);
+}
+
+// The reduce + epilogue of W (1 or 4) consecutive outputs (b, m, n..n+W-1): the splits' fp32
+// partial slabs summed in split order (the same order, so the same bits, wherever it runs),
+// then alpha, bias, beta * C, ReLU, the ReLU mask; the A row sums' split partials folded by the
+// thread of column 0.
+template <typename O, int W>
+__device__ __forceinline__ void reduce_outputs(const GemmParams& p, int b, int m, int n) {
+  const int nb = p.batch0 * p.batch1;
+  const int64_t per = (int64_t)p.M * p.N;
+  const int64_t mn = (int64_t)m * p.N + n;
+  float v[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) v[i] = 0.f;
+  const int64_t sstride = (int64_t)nb * per;
+  const float* src0 = p.ws + (int64_t)b * per + mn;
+  int s = 0;
+  if constexpr (W == 4) {
+    // four slab loads in flight per step, summed in split order
+    for (; s + 4 <= p.splits; s += 4) {
+      float4 t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = *(const float4*)(src0 + (s + u) * sstride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[0] += t[u].x; v[1] += t[u].y; v[2] += t[u].z; v[3] += t[u].w;
+      }
+    }
+  }
+  for (; s < p.splits; ++s) {
+    const float* src = src0 + s * sstride;
+    if constexpr (W == 4) {
+      const float4 t = *(const float4*)src;
+      v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
+    } else {
+      v[0] += *src;
+    }
+  }
+  const int b0 = b / p.batch1, b1 = b % p.batch1;
+  if (p.n_dbias > 0 && n == 0 && p.dbias_tab[b0]) {   // the A row sums' split partials
+    const float* src = p.dbias_ws + (int64_t)b * p.M + m;
+    float r = 0.f;
+    for (int t = 0; t < p.splits; ++t) r += src[(int64_t)t * nb * p.M];
+    float* d = p.dbias_tab[b0];
+    d[m] = (p.dbias_acc ? d[m] : 0.f) + r;
+  }
+  const float* biasp = p.n_bias > 0 ? p.bias_tab[b0] : p.bias;
+  O* cp;
+  int64_t cbase;
+  if (p.c_mode == 1) {
+    cp = (O*)p.c_ptr[b0];
+    cbase = (int64_t)b1 * p.sC1;
+  } else {
+    cp = (O*)p.c_ptr[0];
+    cbase = (int64_t)b0 * p.sC0 + (int64_t)b1 * p.sC1;
+  }
+  const int64_t co = cbase + (int64_t)m * p.ldc + n;
+  const O* auxp = (const O*)p.aux;
+  float cin[W], ain[W];
+  if constexpr (W == 4) {
+    if (p.beta != 0.f) load4_guard(cp + co, 0, 4, true, cin);
+    if (auxp) load4_guard(auxp + cbase + (int64_t)m * p.ldaux + n, 0, 4, true, ain);
+  } else {
+    if (p.beta != 0.f) cin[0] = to_f(cp[co]);
+    if (auxp) ain[0] = to_f(auxp[cbase + (int64_t)m * p.ldaux + n]);
+  }
+  O out[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    float x = v[i] * p.alpha;
+    if (p.bias_mode == 1) x += biasp[n + i];
+    else if (p.bias_mode == 2) x += biasp[m];
+    if (p.beta != 0.f) x += p.beta * cin[i];
+    if (p.relu) x = fmaxf(x, 0.f);
+    if (auxp && !(ain[i] > 0.f)) x = 0.f;
+    out[i] = from_f<O>(x);
+  }
+  if constexpr (W == 4) {
+    if constexpr (sizeof(O) == 4) *(float4*)(cp + co) = *(const float4*)out;
+    else *(uint2*)(cp + co) = *(const uint2*)out;
+  } else {
+    cp[co] = out[0];
+  }
+}
+
+// split-K inside the launch: after writing its partial slab, each split block of an output tile
+// takes a ticket on the tile's counter; the block that draws the last one reduces the tile
+// (reduce_outputs, split order: the bits of splitk_reduce_kernel).  Publication per
+// cdna_hip_programming.md §5 'Projection GEMM at M = 256' item 2 / Guideline 16: every wave
+// drains its slab stores (vmcnt(0)), a block barrier, lane 0's agent-scope release, vmcnt(0)
+// (hipcc may drop the fence's own), the relaxed agent fetch_add; the last arriver's lane 0 does
+// the agent-scope acquire + vmcnt(0) before a barrier and the slab loads.  Any placement of a
+// tile's splits over CUs / XCDs is correct; the counters are zeroed by a memset node ahead of
+// the launch.  Replaces a separate reduce launch that ran 10-90 us per weight gradient in the
+// step (profiles/r04/step_trace_g8.txt).
+template <typename O, class C>
+__device__ __forceinline__ void splitk_fixup(const GemmParams& p, const GemmWork& wk) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  volatile int* flag = (volatile int*)smem;
+  if (threadIdx.x == 0) {
+    const int tile = (wk.b * p.tiles_m + wk.m0 / C::BM) * p.tiles_n + wk.n0 / C::BN;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == p.splits - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  const bool v4 = p.N % 4 == 0 && p.c_vec4;
+  const int mrows = min(C::BM, p.M - wk.m0), ncols = min(C::BN, p.N - wk.n0);
+  if (v4) {
+    const int nq = ncols / 4;                          // ncols % 4 == 0 (N, n0 multiples of 4)
+    for (int e = threadIdx.x; e < mrows * nq; e += C::NT) {
+      const int r = e / nq, q = e - r * nq;
+      reduce_outputs<O, 4>(p, wk.b, wk.m0 + r, wk.n0 + 4 * q);
+    }
+  } else {
+    for (int e = threadIdx.x; e < mrows * ncols; e += C::NT) {
+      const int r = e / ncols, q = e - r * ncols;
+      reduce_outputs<O, 1>(p, wk.b, wk.m0 + r, wk.n0 + q);
+    }
+  }
 }
 
 // split-K reduction + epilogue.  Vector form (N % 4 == 0, C 4-element aligned): one thread per 4
@@ -474,88 +608,15 @@ void gemm_kernel(GemmParams p) {
 template <typename O, bool V4>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   constexpr int W = V4 ? 4 : 1;
-  const int nb = p.batch0 * p.batch1;
   const int64_t per = (int64_t)p.M * p.N;
-  const int64_t total = per * nb / W;
+  const int64_t total = per * p.batch0 * p.batch1 / W;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t idx = e * W;
     const int b = (int)(idx / per);
     const int64_t mn = idx - (int64_t)b * per;
     const int m = (int)(mn / p.N), n = (int)(mn - (int64_t)m * p.N);
-    float v[W];
-#pragma unroll
-    for (int i = 0; i < W; ++i) v[i] = 0.f;
-    const int64_t sstride = (int64_t)nb * per;
-    const float* src0 = p.ws + (int64_t)b * per + mn;
-    int s = 0;
-    if constexpr (V4) {
-      // four slab loads in flight per step, summed in split order (the same order, and so the
-      // same bits, as one at a time)
-      for (; s + 4 <= p.splits; s += 4) {
-        float4 t[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) t[u] = *(const float4*)(src0 + (s + u) * sstride);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          v[0] += t[u].x; v[1] += t[u].y; v[2] += t[u].z; v[3] += t[u].w;
-        }
-      }
-    }
-    for (; s < p.splits; ++s) {
-      const float* src = src0 + s * sstride;
-      if constexpr (V4) {
-        const float4 t = *(const float4*)src;
-        v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
-      } else {
-        v[0] += *src;
-      }
-    }
-    const int b0 = b / p.batch1, b1 = b % p.batch1;
-    if (p.n_dbias > 0 && n == 0 && p.dbias_tab[b0]) {   // the A row sums' split partials
-      const float* src = p.dbias_ws + (int64_t)b * p.M + m;
-      float r = 0.f;
-      for (int t = 0; t < p.splits; ++t) r += src[(int64_t)t * nb * p.M];
-      float* d = p.dbias_tab[b0];
-      d[m] = (p.dbias_acc ? d[m] : 0.f) + r;
-    }
-    const float* biasp = p.n_bias > 0 ? p.bias_tab[b0] : p.bias;
-    O* cp;
-    int64_t cbase;
-    if (p.c_mode == 1) {
-      cp = (O*)p.c_ptr[b0];
-      cbase = (int64_t)b1 * p.sC1;
-    } else {
-      cp = (O*)p.c_ptr[0];
-      cbase = (int64_t)b0 * p.sC0 + (int64_t)b1 * p.sC1;
-    }
-    const int64_t co = cbase + (int64_t)m * p.ldc + n;
-    const O* auxp = (const O*)p.aux;
-    float cin[W], ain[W];
-    if constexpr (V4) {
-      if (p.beta != 0.f) load4_guard(cp + co, 0, 4, true, cin);
-      if (auxp) load4_guard(auxp + cbase + (int64_t)m * p.ldaux + n, 0, 4, true, ain);
-    } else {
-      if (p.beta != 0.f) cin[0] = to_f(cp[co]);
-      if (auxp) ain[0] = to_f(auxp[cbase + (int64_t)m * p.ldaux + n]);
-    }
-    O out[W];
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-      float x = v[i] * p.alpha;
-      if (p.bias_mode == 1) x += biasp[n + i];
-      else if (p.bias_mode == 2) x += biasp[m];
-      if (p.beta != 0.f) x += p.beta * cin[i];
-      if (p.relu) x = fmaxf(x, 0.f);
-      if (auxp && !(ain[i] > 0.f)) x = 0.f;
-      out[i] = from_f<O>(x);
-    }
-    if constexpr (V4) {
-      if constexpr (sizeof(O) == 4) *(float4*)(cp + co) = *(const float4*)out;
-      else *(uint2*)(cp + co) = *(const uint2*)out;
-    } else {
-      cp[co] = out[0];
-    }
+    reduce_outputs<O, W>(p, b, m, n);
   }
 }
 
@@ -736,9 +797,19 @@ extern "C" int jmt_gemm_plan_splits(int ab_dtype, int M, int N, int K, int batch
   return splits;
 }
 
+// split-K workspace: the fp32 partial slabs, then one arrival counter per (batch, output tile)
+// for the in-launch reduction (sized for the smallest tile, 128 x 128)
+static size_t splitk_slab_bytes(int M, int N, int batch, int splits) {
+  return (size_t)splits * (size_t)batch * (size_t)M * (size_t)N * sizeof(float);
+}
+static size_t splitk_counter_bytes(int M, int N, int batch) {
+  const size_t n = (size_t)((M + 127) / 128) * (size_t)((N + 127) / 128) * (size_t)batch;
+  return (n * sizeof(int) + 255) / 256 * 256;
+}
+
 extern "C" size_t jmt_gemm_workspace_bytes(int M, int N, int batch, int splits) {
   if (splits <= 1) return 0;
-  return (size_t)splits * (size_t)batch * (size_t)M * (size_t)N * sizeof(float);
+  return splitk_slab_bytes(M, N, batch, splits) + splitk_counter_bytes(M, N, batch);
 }
 
 extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
@@ -881,12 +952,30 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   p.tiles_m = (d->M + bm - 1) / bm;
   p.tiles_n = (d->N + bn - 1) / bn;
   hipStream_t st = as_stream(stream);
+  // JMT_SPLITK_FUSED=1: split-K reduced by the last-arriving split block of each tile
+  // (splitk_fixup, bit-identical to the separate reduce launch).  Off by default: every tile of a
+  // weight-gradient GEMM finishes in the last wave, so the fused reductions run on one CU per tile
+  // at the end of the launch — TN b3 512x512x19200 58 -> 93 us, the step 4.65 -> 5.43 ms
+  // (profiles/r04/splitk_fused_ab.txt) — where the separate launch spreads them over every CU.
+  static int fused_env = -1;
+  if (fused_env < 0) {
+    const char* e = getenv("JMT_SPLITK_FUSED");
+    fused_env = (e && e[0] == '1') ? 1 : 0;
+  }
+  p.counters = nullptr;
+  if (splits > 1 && fused_env) {
+    p.counters = (int*)((char*)d->workspace + splitk_slab_bytes(d->M, d->N, batch0 * batch1,
+                                                                splits));
+    const size_t cb = (size_t)p.tiles_m * p.tiles_n * batch0 * batch1 * sizeof(int);
+    if (hipMemsetAsync(p.counters, 0, cb, st) != hipSuccess)
+      return set_error(JMT_ERR_HIP, "jmt_gemm: counter memset failed");
+  }
   dim3 grid(p.tiles_m * p.tiles_n, batch0 * batch1, splits);
   if (dt == JMT_F32) launch_t<float>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
   else if (dt == JMT_BF16) launch_t<__bf16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
   else launch_t<_Float16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
   JMT_LAUNCH_CHECK("jmt_gemm");
-  if (splits > 1) {
+  if (splits > 1 && !p.counters) {
     const bool v4 = d->N % 4 == 0 && p.c_vec4;
     const int64_t total = (int64_t)d->M * d->N * batch0 * batch1 / (v4 ? 4 : 1);
     int blocks = (int)((total + 255) / 256);

@@ -40,6 +40,9 @@ struct GemmParams {
   float* dbias_tab[MAXP];
   float* dbias_ws;
   int n_dbias, dbias_acc;
+  // split-K reduced inside the launch (splitk_fixup): per (batch, tile) arrival counters, zeroed
+  // before the launch; nullptr = the separate splitk_reduce_kernel
+  int* counters;
 };
 
 // PF: A-fragment prefetch distance in MFMA rows; PRIO: s_setprio(1) around each MFMA row;

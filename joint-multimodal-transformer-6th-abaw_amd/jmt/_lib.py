@@ -100,6 +100,9 @@ _PROTOS = {
                                 c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
                                 c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_f,
                                 c_vp]),
+    "jmt_attn_dkdv": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_i64, c_vp,
+                              c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                              c_i64, c_vp]),
     "jmt_noop": (c_int, [c_vp]),
     "jmt_small_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
                                    c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,

@@ -927,6 +927,21 @@ def attn_backward(saved, go, dq, dk, dv):
                      c=[_ptr(C, c0)], ldc=C.stride(0), sC=(C.stride(1), dh), batch0=N,
                      batch1=H, device=dev)
         return
+    if (fused and ops._attn_dkdv["on"] and _small_aligned(dk, kcol, cd)
+            and _small_aligned(dv, vcol, cd)):
+        # P and dS (rows of 64-key tiles) -> dK = dS^T Q and dV = P^T dO in one persistent kernel
+        ldp = ops.attn_dkdv_ldp(Lk)
+        P = torch.empty(N * H * Lq * ldp, dtype=cd, device=dev)
+        dS = torch.empty(N * H * Lq * ldp, dtype=cd, device=dev)
+        ops.attn_bwd(_dc(cd), N, H, Lq, Lk, dh, go.data_ptr(), (so_l, so_n),
+                     o.data_ptr(), (o.stride(0), o.stride(1)),
+                     _ptr(q_src, qcol), (sq_l, sq_n), _ptr(k_src, kcol), (sk_l, sk_n),
+                     _ptr(v_src, vcol), (sv_l, sv_n), lse, P, dS, ldp,
+                     _ptr(dq, qcol), (dq.stride(0), dq.stride(1)), scale)
+        ops.attn_dkdv(_dc(cd), N, H, Lq, Lk, dh, P, dS, ldp, go.data_ptr(), (so_l, so_n),
+                      _ptr(q_src, qcol), (sq_l, sq_n), _ptr(dk, kcol),
+                      (dk.stride(0), dk.stride(1)), _ptr(dv, vcol), (dv.stride(0), dv.stride(1)))
+        return
     bS = (H * Lq * ldS, Lq * ldS)
     dS = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)
     if fused:

@@ -277,6 +277,29 @@ def attn_bwd(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k_ptr, 
             launch)
 
 
+_attn_dkdv = {"on": os.environ.get("JMT_ATTN_DKDV", "1") != "0"}
+
+
+def attn_dkdv_ldp(Lk: int) -> int:
+    """P / dS row stride jmt_attn_dkdv reads (whole 64-key tiles)."""
+    return (Lk + 63) // 64 * 64
+
+
+def attn_dkdv(dtype, N, H, Lq, Lk, dh, p, ds, ldp, go_ptr, sgo, q_ptr, sq, dk_ptr, sdk, dv_ptr,
+              sdv):
+    """dV = P^T dO and dK = dS^T Q per (n, h) from attn_bwd's P / dS (ldp >= attn_dkdv_ldp(Lk));
+    one persistent kernel in place of two batched TN GEMMs (off with JMT_ATTN_DKDV=0)."""
+    launch = lambda: _lib.call("jmt_attn_dkdv", dtype, N, H, Lq, Lk, dh, p.data_ptr(),
+                               ds.data_ptr(), ldp, go_ptr, sgo[0], sgo[1], q_ptr, sq[0], sq[1],
+                               dk_ptr, sdk[0], sdk[1], dv_ptr, sdv[0], sdv[1], stream())
+    # algorithmic: the two products; bytes: P, dS (64-key tiles), dO and Q read once per head,
+    # dK and dV written
+    es = 4 if dtype == F32 else 2
+    _hooked({"family": "attn_dkdv", "flops": 4.0 * N * H * Lq * Lk * dh,
+             "bytes": float(N * H) * ((2 * Lq + 2 * Lk) * dh * es +
+                                      2 * Lq * attn_dkdv_ldp(Lk) * es)}, launch)
+
+
 def attn_short_ok(dtype: int, dh: int, Lq: int, Lk: int) -> bool:
     """Shapes the one-block-per-sequence fused kernels cover (jmt_attn_short_*: 16-bit, dh = 512,
     Lq, Lk <= 32); off with JMT_ATTN_FUSED=0 or JMT_ATTN_SHORT=0 (A/B switch)."""

@@ -544,6 +544,99 @@ def test_fused_attention_bwd_vs_fp32(cd, Lq, Lk, N):
     assert torch.isnan(dq[..., :E].float()).all() and torch.isnan(dq[..., 2 * E:].float()).all()
 
 
+def test_gemm_splitk_fused_reduce_bit_identical(tmp_path):
+    """JMT_SPLITK_FUSED=1 (the last split block of each tile reduces it, gemm.hip splitk_fixup)
+    writes bit-identical outputs to the separate reduce launch; both run as child processes
+    (the switch is read once per process)."""
+    import subprocess
+    import sys
+    script = os.path.join(os.path.dirname(__file__), "_splitk_eq.py")
+    f = str(tmp_path / "sk.pt")
+    env = dict(os.environ, JMT_SPLITK_FUSED="1")
+    r = subprocess.run([sys.executable, script, "save", f], env=env, capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    env["JMT_SPLITK_FUSED"] = "0"
+    r = subprocess.run([sys.executable, script, "cmp", f], env=env, capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("Lq,Lk,N,H", [(300, 300, 3, 1), (1024, 1024, 1, 1), (77, 130, 2, 2),
+                                       (33, 20, 3, 1), (1, 65, 2, 1), (129, 1, 2, 1),
+                                       # more (n, h, key-tile) items than CUs: persistent grid
+                                       (300, 300, 64, 2), (40, 200, 100, 1)])
+def test_attn_dkdv_vs_fp32(cd, Lq, Lk, N, H):
+    """jmt_attn_dkdv (attn_dkdv.hip): dV = P^T dO and dK = dS^T Q per (n, h) vs fp32 products of
+    the same 16-bit inputs.  P / dS columns past Lk hold NaN (they may feed only keys that are
+    not stored), outputs land in a packed (Lk, N, 3 E) buffer whose other columns must stay
+    untouched, and the ragged query / key tails cover the clamped rows and the dropped stores."""
+    E = 512 * H
+    g = torch.Generator(device=DEV).manual_seed(31)
+    ldp = ops.attn_dkdv_ldp(Lk)
+    P = torch.full((N * H, Lq, ldp), float("nan"), device=DEV, dtype=cd)
+    dS = torch.full((N * H, Lq, ldp), float("nan"), device=DEV, dtype=cd)
+    P[..., :Lk] = torch.rand(N * H, Lq, Lk, device=DEV, generator=g).to(cd)
+    dS[..., :Lk] = (torch.randn(N * H, Lq, Lk, device=DEV, generator=g) * 0.1).to(cd)
+    qkv = torch.randn(N, Lq, 3 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    go = torch.randn(Lq, N, E, device=DEV, generator=g).to(cd)
+    qv = qkv[..., :E]
+    out = torch.full((N, Lk, 3 * E), 7.0, device=DEV, dtype=cd).permute(1, 0, 2)
+    dk, dv = out[..., E:2 * E], out[..., 2 * E:]
+    st = lambda t: (t.stride(0), t.stride(1))
+    ops.attn_dkdv(ops.dt(qkv), N, H, Lq, Lk, 512, P, dS, ldp, go.data_ptr(), st(go),
+                  qv.data_ptr(), st(qkv), dk.data_ptr(), st(out), dv.data_ptr(), st(out))
+    torch.cuda.synchronize()
+    Pr = P[..., :Lk].float().view(N, H, Lq, Lk)
+    dSr = dS[..., :Lk].float().view(N, H, Lq, Lk)
+    gor = go.float().view(Lq, N, H, 512)
+    qr = qv.float().reshape(Lq, N, H, 512)
+    dvr = torch.einsum("nhqk,qnhd->knhd", Pr, gor).reshape(Lk, N, E)
+    dkr = torch.einsum("nhqk,qnhd->knhd", dSr, qr).reshape(Lk, N, E)
+    u = 2.0 ** -8 if cd == torch.bfloat16 else 2.0 ** -11
+    for got, ref in ((dv, dvr), (dk, dkr)):
+        assert torch.isfinite(got.float()).all()
+        err = (got.float() - ref).abs().max().item()
+        # fp32 accumulation of Lq products; the result rounded once to 16 bits
+        assert err <= 2 * u * ref.abs().max().item() + 1e-6 * Lq, (err, ref.abs().max().item())
+    assert (out[..., :E].float() == 7.0).all()
+
+
+@pytest.mark.parametrize("Lq,Lk,N", [(300, 300, 4), (70, 129, 3)])
+def test_attention_backward_dkdv_matches_gemm_path(Lq, Lk, N):
+    """functional.attn_backward: the jmt_attn_dkdv path (default) and the two-GEMM path
+    (JMT_ATTN_DKDV=0) give the same dQ and agree on dK / dV within fp32-accumulation noise
+    (the same rounded P / dS feed both)."""
+    from jmt import functional as F
+    cd = torch.bfloat16
+    E, H = 512, 1
+    g = torch.Generator(device=DEV).manual_seed(32)
+    qkv = torch.randn(N, Lq, 3 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    kv = torch.randn(N, Lk, 2 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    F.set_compute_dtype(cd)
+    try:
+        o, saved = F.attn_forward(qkv, kv, kv, E, H, 0, 0, E)
+    finally:
+        F.set_compute_dtype(None)
+    go = torch.randn(Lq, N, E, device=DEV, generator=g).to(cd)
+    res = []
+    for on in (True, False):
+        ops._attn_dkdv["on"] = on
+        try:
+            dq = torch.zeros(N, Lq, 3 * E, device=DEV, dtype=cd).permute(1, 0, 2)
+            dkv = torch.zeros(N, Lk, 2 * E, device=DEV, dtype=cd).permute(1, 0, 2)
+            F.attn_backward(saved, go, dq, dkv, dkv)
+            torch.cuda.synchronize()
+            res.append((dq.float().clone(), dkv.float().clone()))
+        finally:
+            ops._attn_dkdv["on"] = True
+    assert torch.equal(res[0][0], res[1][0])
+    ref = res[1][1]
+    err = (res[0][1] - ref).abs().max().item()
+    assert err <= 2 * 2.0 ** -8 * ref.abs().max().item(), err
+
+
 def test_fused_attention_forced_rescale():
     """The lazy-rescale branch of the forward (a row max rising > 8 log2 units after the first
     tile) must be exact: one key in the third 64-key tile is spiked to dominate one query row
