@@ -216,7 +216,7 @@ int jmt_attn_bwd_km(int dt, int N, int H, int Lq, int Lk, int dh, const void* go
 
 /* Key-side attention gradients from the handed-over probabilities (round 4): per (n, h)
  * dV = P^T dO and dK = dS^T Q, P / dS as jmt_attn_bwd writes them (row (n*H + h)*Lq + q, keys in
- * columns, row stride ldp >= 64 ceil(Lk / 64): the kernel reads whole 64-key tiles; columns past
+ * columns, row stride ldp >= 128 ceil(Lk / 128): the kernel reads whole 128-key tiles; columns past
  * Lk only feed outputs that are not stored).  dO / Q / dK / dV seq-first views as jmt_attn_bwd's
  * operands (row stride s*_l, batch stride s*_n, head h at columns 512 h).  16-bit, dh = 512.
  * Replaces the two batched TN jmt_gemm calls (M = Lk, N = dh, K = Lq) of the same products. */

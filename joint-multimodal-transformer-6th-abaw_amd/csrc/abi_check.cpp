@@ -100,10 +100,10 @@ int main() {
   expect_err("attn_bwd sizes", jmt_attn_bwd(JMT_BF16, -1, 1, 300, 300, 512, misal, 1, 1, misal, 1,
                                             1, misal, 1, 1, misal, 1, 1, misal, 1, 1, fnull,
                                             misal, misal, 8, misal, 1, 1, 0.1f, nullptr));
-  expect_err("attn_dkdv ldp", jmt_attn_dkdv(JMT_BF16, 2, 1, 300, 300, 512, misal, misal, 304,
+  expect_err("attn_dkdv ldp", jmt_attn_dkdv(JMT_BF16, 2, 1, 300, 300, 512, misal, misal, 320,
                                            misal, 512, 512, misal, 512, 512, misal, 512, 512,
                                            misal, 512, 512, nullptr));
-  expect_err("attn_dkdv head dim", jmt_attn_dkdv(JMT_BF16, 2, 1, 300, 300, 64, misal, misal, 320,
+  expect_err("attn_dkdv head dim", jmt_attn_dkdv(JMT_BF16, 2, 1, 300, 300, 64, misal, misal, 384,
                                                  misal, 512, 512, misal, 512, 512, misal, 512,
                                                  512, misal, 512, 512, nullptr));
   expect_err("small_attn_fwd null", jmt_small_attn_fwd(JMT_BF16, 4, 1, 6, 6, 512, nullptr, 512,

@@ -7,35 +7,44 @@
 // Reference: the dK / dV of autograd's backward of F.multi_head_attention_forward behind every
 // nn.MultiheadAttention of mm_multi_transformers.py:57,142-167.
 //
-// Geometry: an item is (n, h, 64-key tile); a block (8 waves, one per CU, persistent over items
-// with attn.hip's XCD-contiguous item ranges, so the key tiles of one head share its dO / Q rows in
-// one L2) streams the queries in chunks of 32:
-//  * stage = dO rows, Q rows (32 x 1 KiB each, the swizzled row image of attn_common.h) and the
-//    P / dS tile (32 queries x 64 keys, 128-B rows, 16-B chunk c of row r at c ^ ((r >> 1 & 3) << 1):
-//    the transposed reads below are conflict-free) = 72 KiB, double-buffered (144 KiB), filled by
-//    LDS-DMA issued from inline asm (every wait explicit) one chunk ahead, across items too;
-//  * waves 0-3 compute dV, waves 4-7 dK, wave w the 128 head dims 128 (w & 3) ..: per chunk one
-//    MFMA k-step of 16x16x32 over 4 key groups x 8 dim groups (128 accumulator registers).  Both
-//    operands come from ds_read_b64_tr_b16 reads (the dims of dO / Q and the keys of P / dS are
-//    columns of their images), in the k-slot order of attn.hip's P V product;
+// Geometry: an item is (n, h, product, 128-key tile) — the product (dV from P and dO, or dK from
+// dS and Q) is part of the item, so a block holds one product's 128 x 512 fp32 accumulator (128
+// registers per wave) and streams one row operand: per 128 keys it fetches Lq x (1 KiB + 256 B)
+// (the two-product 64-key item of the first version fetched Lq x (2 KiB + 256 B) per 64 keys and
+// ran at 2.9 TB/s of LDS fill: profiles/r04/dkdv_v1_vs_gemm.jsonl).  Blocks are persistent (one
+// per CU, attn.hip's XCD-contiguous item ranges: the key tiles of one head and product share its
+// dO / Q rows in one L2) and stream the queries in chunks of 32:
+//  * stage = 32 dO / Q rows (1 KiB each, the swizzled row image of attn_common.h) and the P / dS
+//    tile of those rows (32 x 128 keys, 256-B rows, 16-B chunk c of row r at c ^ ((r & 7) << 1):
+//    conflict-free transposed reads) = 40 KiB; 4 stages (160 KiB), filled by LDS-DMA from inline
+//    asm three chunks ahead, across items too; every wait is an exact vmcnt;
+//  * wave w owns head dims 64 w .. +63: per chunk one MFMA k-step of 16x16x32 over 8 key groups x
+//    4 dim groups.  Both operands come from ds_read_b64_tr_b16 reads (the dims of dO / Q and the
+//    keys of P / dS are columns of their images), in the k-slot order of attn.hip's P V product;
 //  * queries past Lq (the last chunk) read a clamped row and are zeroed in the P / dS fragment;
 //    keys past Lk compute on whatever the P / dS row holds there and are not stored;
 //  * the accumulators go straight from registers to HBM (16-B buffer stores of paired subtiles;
 //    the buffer range check drops rows past Lk, so every wave issues exactly 16 stores per item
-//    and the next item's first wait can leave them in flight).
-// HBM bytes per (n, h): Lq rows of dO and Q (1 KiB each; once per head when its key tiles share
-// the L2), Lq x 64 ceil(Lk / 64) x 2 B of P and of dS, Lk rows of dK and dV written.
+//    and the waits that follow count them).
+// HBM bytes per (n, h): Lq rows of dO and of Q (1 KiB each; once per head when its key tiles share
+// the L2), Lq x 128 ceil(Lk / 128) x 2 B of P and of dS, Lk rows of dK and of dV written.
 #include "attn_common.h"
 
 namespace jmt {
 
-constexpr int DK_KT = 64;                               // keys per item
+constexpr int DK_KT = 128;                              // keys per item
 constexpr int DK_QC = 32;                               // queries per chunk (one MFMA k-step)
 constexpr int DK_PROW = 2 * DK_KT;                      // P / dS image row bytes
 constexpr int DK_IMG = DK_QC * AT_ROWB;                 // dO or Q image (32 KiB)
-constexpr int DK_PIMG = DK_QC * DK_PROW;                // P or dS image (4 KiB)
-constexpr int DK_STAGE = 2 * DK_IMG + 2 * DK_PIMG;      // 72 KiB
-constexpr int DK_LDS = 2 * DK_STAGE;                    // 144 KiB
+constexpr int DK_PIMG = DK_QC * DK_PROW;                // P or dS image (8 KiB)
+constexpr int DK_STAGE = DK_IMG + DK_PIMG;              // 40 KiB
+#ifndef JMT_DKDV_NS
+#define JMT_DKDV_NS 4                                   // (dev A/B: 3 -> 120 KiB)
+#endif
+constexpr int DK_NS = JMT_DKDV_NS;                      // stages
+constexpr int DK_LDS = DK_NS * DK_STAGE;                // 160 KiB
+static_assert(DK_NS >= 2 && DK_NS <= 4, "2-4 stages (the wait table covers 0-2 later stages)");
+constexpr int DK_NDMA = DK_QC / 8 + 1;                  // DMA wave-instructions per wave per stage
 constexpr int DK_NST = 16;                              // output stores per wave per item
 
 struct AttnDkdvArgs {
@@ -51,34 +60,74 @@ struct AttnDkdvArgs {
 
 // byte offset of 16-B chunk `c` of row `r` of a P / dS image
 __device__ __forceinline__ int pimg_off(int r, int c) {
-  return r * DK_PROW + ((c ^ (((r >> 1) & 3) << 1)) << 4);
+  return r * DK_PROW + ((c ^ ((r & 7) << 1)) << 4);
 }
 
-// one stage: dO and Q rows q0 .. q0+31 (clamped to Lq - 1), the P (waves 0-3) / dS (waves 4-7)
-// tile of those rows, keys k0 .. k0+63: 4 + 4 + 1 DMA wave-instructions per wave
+// item -> (n H + h, n, h, product (0: dV, 1: dK), first key)
+struct DkItem {
+  int nh, n, hd, role, k0;
+};
+__device__ __forceinline__ DkItem dk_decode(const AttnDkdvArgs& a, int it) {
+  DkItem d;
+  const int t = it / a.nkt;
+  d.k0 = (it - t * a.nkt) * DK_KT;
+  d.nh = t >> 1;
+  d.role = t & 1;
+  d.n = d.nh / a.H;
+  d.hd = d.nh - d.n * a.H;
+  return d;
+}
+
+// one stage: rows q0 .. q0+31 (clamped to Lq - 1) of dO or Q, and of the P or dS tile (keys
+// k0 .. k0+127): 4 + 1 DMA wave-instructions per wave.  Row offsets in 32-bit byte arithmetic
+// from a per-head base (the host checks Lq rows fit): the 64-bit row products of stage_rows cost
+// ~25 scalar instructions per DMA, and the CU's one scalar unit serves all 8 waves.
 template <typename T>
-__device__ __forceinline__ void dkdv_stage(char* st, const AttnDkdvArgs& a, int nh, int n, int hd,
-                                           int k0, int q0) {
+__device__ __forceinline__ void dkdv_stage(char* st, const AttnDkdvArgs& a, const DkItem& d,
+                                           int q0) {
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  stage_rows<T, DK_QC, 8, true>(st, (const T*)a.go + (int64_t)n * a.sgo_n + hd * AT_DH, a.sgo_l,
-                                q0, a.Lq);
-  stage_rows<T, DK_QC, 8, true>(st + DK_IMG, (const T*)a.q + (int64_t)n * a.sq_n + hd * AT_DH,
-                                a.sq_l, q0, a.Lq);
-  const int i = wu & 3;
-  const int r = 8 * i + (lane >> 3);                    // image row of this lane's 16 B
-  const int cs = (lane & 7) ^ (((r >> 1) & 3) << 1);    // the logical chunk it holds
+  const char* rb;
+  int ldb;
+  if (d.role == 0) {
+    rb = (const char*)((const T*)a.go + (int64_t)d.n * a.sgo_n + d.hd * AT_DH);
+    ldb = (int)(a.sgo_l * (int64_t)sizeof(T));
+  } else {
+    rb = (const char*)((const T*)a.q + (int64_t)d.n * a.sq_n + d.hd * AT_DH);
+    ldb = (int)(a.sq_l * (int64_t)sizeof(T));
+  }
+#pragma unroll
+  for (int i = 0; i < DK_QC / 8; ++i) {
+    const int r = wu * (DK_QC / 8) + i;
+    const int src = min(q0 + r, a.Lq - 1);
+    const unsigned off = (unsigned)(lane ^ ((r & 7) << 1)) << 4;
+    glds16_asm(rb + (unsigned)(src * ldb) + off, st + r * AT_ROWB);
+  }
+  const int r = 4 * wu + (lane >> 4);                   // P / dS image row of this lane's 16 B
+  const int cs = (lane & 15) ^ ((r & 7) << 1);          // the logical chunk it holds
   const int src_row = min(q0 + r, a.Lq - 1);
-  JMT_DCHECK(src_row >= 0 && k0 + 8 * cs + 8 <= a.ldp);
-  const T* src = (const T*)(wu < 4 ? a.p : a.ds) + ((int64_t)nh * a.Lq + src_row) * a.ldp + k0 +
-                 8 * cs;
-  glds16_asm(src, st + 2 * DK_IMG + (wu >> 2) * DK_PIMG + i * 1024);
+  JMT_DCHECK(src_row >= 0 && d.k0 + 8 * cs + 8 <= a.ldp);
+  const char* pb = (const char*)((const T*)(d.role == 0 ? a.p : a.ds) +
+                                 (int64_t)d.nh * a.Lq * a.ldp + d.k0);
+  glds16_asm(pb + (unsigned)(src_row * (int)(a.ldp * sizeof(T))) + 16 * cs,
+             st + DK_IMG + wu * 1024);
 }
 
-// s_waitcnt vmcnt(n) for the few counts the item loop needs
-__device__ __forceinline__ void dkdv_wait(int n) {
-  if (n == 0) wait_vmcnt<0>();
-  else wait_vmcnt<DK_NST>();
+// s_waitcnt vmcnt(stages * DK_NDMA + stores * DK_NST) for the counts the chunk loop meets:
+// 0-2 later stages and 0-3 items' output stores in flight behind the awaited stage
+template <int S>
+__device__ __forceinline__ void dkdv_wait_s(int stores) {
+  switch (stores) {
+    case 0: wait_vmcnt<S * DK_NDMA>(); break;
+    case 1: wait_vmcnt<S * DK_NDMA + DK_NST>(); break;
+    case 2: wait_vmcnt<S * DK_NDMA + 2 * DK_NST>(); break;
+    default: wait_vmcnt<S * DK_NDMA + 3 * DK_NST>(); break;
+  }
+}
+__device__ __forceinline__ void dkdv_wait(int stages, int stores) {
+  if (stages == 0) dkdv_wait_s<0>(stores);
+  else if (stages == 1) dkdv_wait_s<1>(stores);
+  else dkdv_wait_s<2>(stores);
 }
 
 template <typename T>
@@ -89,57 +138,64 @@ __global__ __launch_bounds__(512, 2) void attn_dkdv_kernel(AttnDkdvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int role = w >> 2, dq = w & 3;                  // role 0: dV from P, dO; 1: dK from dS, Q
   const int nqc = (a.Lq + DK_QC - 1) / DK_QC;
   int item, iend, istride;
   item_range(a.nitems, item, iend, istride);
   if (item >= iend) return;
 
-  int tb[8], pb[4];                                     // transposed-read lane bases
+  int tb[4], pb[8];                                     // transposed-read lane bases
 #pragma unroll
-  for (int t = 0; t < 8; ++t) tb[t] = tr_base(t, li, g, dq >> 1) + 256 * (dq & 1);
+  for (int t = 0; t < 4; ++t) tb[t] = tr_base(4 * (w & 1) + t, li, g, 0) + 256 * (w >> 1);
 #pragma unroll
-  for (int kg = 0; kg < 4; ++kg)
+  for (int kg = 0; kg < 8; ++kg)
     pb[kg] = pimg_off(4 * g + (li >> 2), 2 * kg + ((li & 3) >> 1)) + 8 * (li & 1);
 
-  auto decode = [&](int it, int& nh, int& n, int& hd, int& k0) {
-    nh = it / a.nkt;
-    n = nh / a.H;
-    hd = nh - n * a.H;
-    k0 = (it - nh * a.nkt) * DK_KT;
+  // issue cursor: the chunk whose stage goes out next (runs DK_NS - 1 chunks ahead of the compute)
+  int is_item = item, is_c = 0;
+  DkItem is_d = dk_decode(a, item);
+  bool is_ok = true;
+  int is_buf = 0;
+  unsigned after = 0;      // 4 bits per buffer: store batches issued after the stage it holds
+  int inflight = 0;        // stages issued and not yet waited for
+  auto issue = [&]() {
+    if (is_ok) {
+      dkdv_stage<T>(smem + is_buf * DK_STAGE, a, is_d, DK_QC * is_c);
+      after &= ~(15u << (4 * is_buf));
+      ++inflight;
+      if (++is_c == nqc) {
+        is_c = 0;
+        is_item += istride;
+        is_ok = is_item < iend;
+        if (is_ok) is_d = dk_decode(a, is_item);
+      }
+    }
+    is_buf = is_buf == DK_NS - 1 ? 0 : is_buf + 1;
   };
-  int nh, n, hd, k0;
-  decode(item, nh, n, hd, k0);
+  for (int i = 0; i < DK_NS - 1; ++i) issue();
   int buf = 0;
-  dkdv_stage<T>(smem, a, nh, n, hd, k0, 0);
-  int nst = 0;                                          // stores issued after this item's stage 0
 
   while (true) {
-    const int nxt = item + istride;
-    const bool more = nxt < iend;
-    int nh2 = 0, n2 = 0, hd2 = 0, k02 = 0;
-    if (more) decode(nxt, nh2, n2, hd2, k02);
-    f32x4 acc[4][8];
+    const DkItem d = dk_decode(a, item);
+    const bool more = item + istride < iend;
+    f32x4 acc[8][4];
 #pragma unroll
-    for (int kg = 0; kg < 4; ++kg)
+    for (int kg = 0; kg < 8; ++kg)
 #pragma unroll
-      for (int t = 0; t < 8; ++t) acc[kg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < 4; ++t) acc[kg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     for (int c = 0; c < nqc; ++c) {
       const char* cur = smem + buf * DK_STAGE;
-      // this chunk's stage landed (only the previous item's output stores may still be in
-      // flight), and every wave is done reading the other buffer
-      dkdv_wait(c == 0 ? nst : 0);
+      // this chunk's stage landed (the later stages and the output stores issued after it may
+      // stay in flight), and every wave is done reading the buffer restaged below
+      dkdv_wait(inflight - 1, (after >> (4 * buf)) & 15);
+      --inflight;
       lds_barrier();
-      if (c + 1 < nqc) dkdv_stage<T>(smem + (buf ^ 1) * DK_STAGE, a, nh, n, hd, k0, DK_QC * (c + 1));
-      else if (more) dkdv_stage<T>(smem + (buf ^ 1) * DK_STAGE, a, nh2, n2, hd2, k02, 0);
-      const char* img = cur + role * DK_IMG;
-      const char* pim = cur + 2 * DK_IMG + role * DK_PIMG;
-      F kf[4];
+      issue();
+      F kf[8];
 #pragma unroll
-      for (int kg = 0; kg < 4; ++kg) {
-        const Hf lo = tr_read<Hf>(pim + pb[kg]);
-        const Hf hi = tr_read<Hf>(pim + pb[kg] + 16 * DK_PROW);
+      for (int kg = 0; kg < 8; ++kg) {
+        const Hf lo = tr_read<Hf>(cur + DK_IMG + pb[kg]);
+        const Hf hi = tr_read<Hf>(cur + DK_IMG + pb[kg] + 16 * DK_PROW);
         kf[kg] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
       const int q0 = DK_QC * c;
@@ -148,62 +204,41 @@ __global__ __launch_bounds__(512, 2) void attn_dkdv_kernel(AttnDkdvArgs a) {
         for (int e = 0; e < 8; ++e) {
           const bool in = q0 + 16 * (e >> 2) + 4 * g + (e & 3) < a.Lq;
 #pragma unroll
-          for (int kg = 0; kg < 4; ++kg) kf[kg][e] = in ? kf[kg][e] : from_f<T>(0.f);
+          for (int kg = 0; kg < 8; ++kg) kf[kg][e] = in ? kf[kg][e] : from_f<T>(0.f);
         }
       }
-      {   // dim subtiles in double-buffered pairs (t = 2 b + i)
-        F fa[2], fb[2];
-        auto dbatch = [&](F* dst, int b) {
+      F df[4];
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const char* ad = img + tb[2 * b + i];
-            const Hf lo = tr_read<Hf>(ad);
-            const Hf hi = tr_read<Hf>(ad + 16 * AT_ROWB);
-            dst[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-          }
-        };
-        dbatch(fa, 0);
-#pragma unroll
-        for (int b = 0; b < 4; b += 2) {
-          dbatch(fb, b + 1);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int kg = 0; kg < 4; ++kg)
-              acc[kg][2 * b + i] = mfma16(fa[i], kf[kg], acc[kg][2 * b + i]);
-          __builtin_amdgcn_sched_barrier(0);
-          if (b + 2 < 4) dbatch(fa, b + 2);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int kg = 0; kg < 4; ++kg)
-              acc[kg][2 * b + 2 + i] = mfma16(fb[i], kf[kg], acc[kg][2 * b + 2 + i]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+      for (int t = 0; t < 4; ++t) {
+        const Hf lo = tr_read<Hf>(cur + tb[t]);
+        const Hf hi = tr_read<Hf>(cur + tb[t] + 16 * AT_ROWB);
+        df[t] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
-      buf ^= 1;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int kg = 0; kg < 8; ++kg) acc[kg][t] = mfma16(df[t], kf[kg], acc[kg][t]);
+      buf = buf == DK_NS - 1 ? 0 : buf + 1;
     }
 
-    // ---- outputs: lane = key k0 + 16 kg + li, dims 128 dq + 16 t + 4 g + r; subtiles t, t + 1
+    // ---- outputs: lane = key k0 + 16 kg + li, dims 64 w + 16 t + 4 g + r; subtiles t, t + 1
     // paired by v_permlane16_swap into 8 consecutive dims per lane (store_acc_direct's scheme)
     {
-      T* ob = role == 0 ? (T*)a.dv + (int64_t)n * a.sdv_n : (T*)a.dk + (int64_t)n * a.sdk_n;
-      const int64_t sl = role == 0 ? a.sdv_l : a.sdk_l;
-      ob += (int64_t)hd * AT_DH + (int64_t)k0 * sl;
+      T* ob = d.role == 0 ? (T*)a.dv + (int64_t)d.n * a.sdv_n : (T*)a.dk + (int64_t)d.n * a.sdk_n;
+      const int64_t sl = d.role == 0 ? a.sdv_l : a.sdk_l;
+      ob += (int64_t)d.hd * AT_DH + (int64_t)d.k0 * sl;
       const uint64_t ba = (uint64_t)(uintptr_t)ob;
       const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)ba);
       const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(ba >> 32));
-      const int nrows = min(DK_KT, a.Lk - k0);
+      const int nrows = min(DK_KT, a.Lk - d.k0);
       const int bytes = __builtin_amdgcn_readfirstlane((int)(nrows * sl * (int64_t)sizeof(T)));
       const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(((uint64_t)bhi << 32) | blo), 0, bytes, 0x00020000);
       const int sl32 = (int)sl;
 #pragma unroll
-      for (int kg = 0; kg < 4; ++kg) {
+      for (int kg = 0; kg < 8; ++kg) {
 #pragma unroll
-        for (int jp = 0; jp < 4; ++jp) {
+        for (int jp = 0; jp < 2; ++jp) {
           uint32_t pk[2][2];
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh)
@@ -215,16 +250,18 @@ __global__ __launch_bounds__(512, 2) void attn_dkdv_kernel(AttnDkdvArgs a) {
             }
           const auto r0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
           const auto r1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
-          const int col = 128 * dq + 16 * (2 * jp + (g & 1)) + 8 * (g >> 1);
+          const int col = 64 * w + 16 * (2 * jp + (g & 1)) + 8 * (g >> 1);
           const u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
           const int off = ((16 * kg + li) * sl32 + col) * (int)sizeof(T);
           __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, 0);
         }
       }
     }
-    nst = DK_NST;
+    // these stores follow the stages in flight (the next two chunks'; the free buffer's count is
+    // reset when it is restaged)
+    after += 0x1111;
     if (!more) break;
-    item = nxt; nh = nh2; n = n2; hd = hd2; k0 = k02;
+    item += istride;
   }
   wait_vmcnt<0>();
 }
@@ -264,27 +301,30 @@ extern "C" int jmt_attn_dkdv(int dt, int N, int H, int Lq, int Lk, int dh, const
     JMT_CHECK_ARG(strides[i] % 8 == 0, "jmt_attn_dkdv: stride %d not a multiple of 8", i);
   const int nkt = (Lk + DK_KT - 1) / DK_KT;
   JMT_CHECK_ARG(ldp >= (int64_t)nkt * DK_KT,
-                "jmt_attn_dkdv: ldp must cover 64-key tiles (>= %d)", nkt * DK_KT);
+                "jmt_attn_dkdv: ldp must cover 128-key tiles (>= %d)", nkt * DK_KT);
   JMT_CHECK_ARG(sdk_l >= H * AT_DH && sdv_l >= H * AT_DH &&
                     (int64_t)DK_KT * sdk_l * 2 < (1LL << 31) &&
                     (int64_t)DK_KT * sdv_l * 2 < (1LL << 31),
                 "jmt_attn_dkdv: dK / dV row stride out of range");
-  JMT_CHECK_ARG((int64_t)N * H * nkt < (1LL << 31), "jmt_attn_dkdv: too many items");
+  JMT_CHECK_ARG((int64_t)N * H * 2 * nkt < (1LL << 31), "jmt_attn_dkdv: too many items");
+  JMT_CHECK_ARG((int64_t)Lq * sgo_l * 2 < (1LL << 31) && (int64_t)Lq * sq_l * 2 < (1LL << 31) &&
+                    (int64_t)Lq * ldp * 2 < (1LL << 31),
+                "jmt_attn_dkdv: Lq rows of dO / Q / P exceed 2 GiB");
   AttnDkdvArgs a = {};
   a.p = p; a.ds = ds; a.go = go; a.q = q; a.dk = dk; a.dv = dv;
   a.ldp = ldp; a.sgo_l = sgo_l; a.sgo_n = sgo_n; a.sq_l = sq_l; a.sq_n = sq_n;
   a.sdk_l = sdk_l; a.sdk_n = sdk_n; a.sdv_l = sdv_l; a.sdv_n = sdv_n;
-  a.Lq = Lq; a.Lk = Lk; a.H = H; a.nkt = nkt; a.nitems = N * H * nkt;
+  a.Lq = Lq; a.Lk = Lk; a.H = H; a.nkt = nkt; a.nitems = N * H * 2 * nkt;
   const dim3 grid(dkdv_grid(a.nitems));
   hipStream_t st = as_stream(stream);
   if (dt == JMT_BF16) {
-    static bool once = (hipFuncSetAttribute((const void*)attn_dkdv_kernel<__bf16>,
+    static bool once = ((void)hipFuncSetAttribute((const void*)attn_dkdv_kernel<__bf16>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, DK_LDS),
                         true);
     (void)once;
     hipLaunchKernelGGL((attn_dkdv_kernel<__bf16>), grid, dim3(512), (size_t)DK_LDS, st, a);
   } else {
-    static bool once = (hipFuncSetAttribute((const void*)attn_dkdv_kernel<_Float16>,
+    static bool once = ((void)hipFuncSetAttribute((const void*)attn_dkdv_kernel<_Float16>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, DK_LDS),
                         true);
     (void)once;

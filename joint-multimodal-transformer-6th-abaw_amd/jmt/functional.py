@@ -929,7 +929,7 @@ def attn_backward(saved, go, dq, dk, dv):
         return
     if (fused and ops._attn_dkdv["on"] and _small_aligned(dk, kcol, cd)
             and _small_aligned(dv, vcol, cd)):
-        # P and dS (rows of 64-key tiles) -> dK = dS^T Q and dV = P^T dO in one persistent kernel
+        # P and dS (rows of 128-key tiles) -> dK = dS^T Q and dV = P^T dO in one persistent kernel
         ldp = ops.attn_dkdv_ldp(Lk)
         P = torch.empty(N * H * Lq * ldp, dtype=cd, device=dev)
         dS = torch.empty(N * H * Lq * ldp, dtype=cd, device=dev)

@@ -281,8 +281,8 @@ _attn_dkdv = {"on": os.environ.get("JMT_ATTN_DKDV", "1") != "0"}
 
 
 def attn_dkdv_ldp(Lk: int) -> int:
-    """P / dS row stride jmt_attn_dkdv reads (whole 64-key tiles)."""
-    return (Lk + 63) // 64 * 64
+    """P / dS row stride jmt_attn_dkdv reads (whole 128-key tiles)."""
+    return (Lk + 127) // 128 * 128
 
 
 def attn_dkdv(dtype, N, H, Lq, Lk, dh, p, ds, ldp, go_ptr, sgo, q_ptr, sq, dk_ptr, sdk, dv_ptr,
@@ -292,7 +292,7 @@ def attn_dkdv(dtype, N, H, Lq, Lk, dh, p, ds, ldp, go_ptr, sgo, q_ptr, sq, dk_pt
     launch = lambda: _lib.call("jmt_attn_dkdv", dtype, N, H, Lq, Lk, dh, p.data_ptr(),
                                ds.data_ptr(), ldp, go_ptr, sgo[0], sgo[1], q_ptr, sq[0], sq[1],
                                dk_ptr, sdk[0], sdk[1], dv_ptr, sdv[0], sdv[1], stream())
-    # algorithmic: the two products; bytes: P, dS (64-key tiles), dO and Q read once per head,
+    # algorithmic: the two products; bytes: P, dS (128-key tiles), dO and Q read once per head,
     # dK and dV written
     es = 4 if dtype == F32 else 2
     _hooked({"family": "attn_dkdv", "flops": 4.0 * N * H * Lq * Lk * dh,

@@ -32,10 +32,14 @@ def time_us(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--shapes", type=int, nargs="*", help="indices into SHAPES")
+    ap.add_argument("--only", choices=["dkdv", "gemm"], help="time one implementation")
     args = ap.parse_args()
     dev = "cuda"
     E = 512
-    for N, L in SHAPES:
+    for i, (N, L) in enumerate(SHAPES):
+        if args.shapes and i not in args.shapes:
+            continue
         g = torch.Generator(device=dev).manual_seed(1)
         ldp = ops.attn_dkdv_ldp(L)
         P = (torch.rand(N, L, ldp, device=dev, generator=g)).bfloat16()
@@ -63,6 +67,8 @@ def main():
         res = {}
         for r in range(2):
             for name, f in (("dkdv", fused), ("gemm", gemms)):
+                if args.only and name != args.only:
+                    continue
                 med, mn = time_us(f, args.reps)
                 res.setdefault(name, []).append(med)
         flops = 4.0 * N * L * L * E
