@@ -496,7 +496,7 @@ def main():
             step()
         torch.cuda.synchronize()
         probe.on = False
-        streams.set_side_enabled(os.environ.get("JMT_SIDE_STREAM", "1") != "0")
+        streams.set_side_enabled(os.environ.get("JMT_SIDE_STREAM", "0") == "1")
         ops.set_launch_hook(None)
     if world > 1:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)

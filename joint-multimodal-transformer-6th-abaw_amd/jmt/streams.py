@@ -15,7 +15,7 @@ import torch
 
 _pool: dict = {}
 _enabled = {"on": True, "capture": os.environ.get("JMT_CAPTURE_STREAMS", "1") != "0",
-            "side": os.environ.get("JMT_SIDE_STREAM", "1") != "0"}
+            "side": os.environ.get("JMT_SIDE_STREAM", "0") == "1"}
 
 
 def set_enabled(on: bool) -> None:

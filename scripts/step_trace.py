@@ -1,7 +1,8 @@
 """Kernels of the timed region of a `rocprofv3 --kernel-trace` run of bench.py: the last
 `--steps` training steps (each ends with the fused SGD launch), per-kernel-kind time per step,
 concurrency (sum of kernel time / wall) and any torch (at::native) kernel inside.
-    python scripts/step_trace.py <run_kernel_trace.csv> [steps]"""
+    python scripts/step_trace.py <run_kernel_trace.csv> [steps] [--seq]
+--seq also lists the last step's launches in order (start offset, duration, grid, kind)."""
 import csv
 import re
 import sys
@@ -20,7 +21,7 @@ def kind(n):
     return k
 
 
-def main(path, steps=10):
+def main(path, steps=10, seq=False):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     sgd = [i for i, r in enumerate(rows) if "sgd" in r["Kernel_Name"]]
@@ -40,7 +41,16 @@ def main(path, steps=10):
         print(f"{us:9.1f} us/step {n / steps:6.1f} launches  {k}")
     torch_k = [r["Kernel_Name"][:90] for r in reg if "at::native" in r["Kernel_Name"]]
     print("torch kernels in the timed region:", len(torch_k), sorted(set(torch_k))[:5])
+    if seq:
+        s0 = sgd[-2] + 1
+        b = int(rows[s0]["Start_Timestamp"])
+        print("last step, in launch order: start_us dur_us grid kind")
+        for r in rows[s0:last + 1]:
+            st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            print(f"{(st - b) / 1e3:9.1f} {(en - st) / 1e3:8.1f} {r.get('Grid_Size', '?'):>9} "
+                  f"{kind(r['Kernel_Name'])}")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 10)
+    args = [a for a in sys.argv[1:] if a != "--seq"]
+    main(args[0], int(args[1]) if len(args) > 1 else 10, "--seq" in sys.argv)

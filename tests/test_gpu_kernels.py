@@ -918,6 +918,7 @@ def test_bounds_build_reports_no_violations():
                        text=True, timeout=240, env=dict(os.environ, JMT_LIB=_BOUNDS_LIB))
     if r.returncode == 5:
         pytest.skip("bounds build predates the library ABI (rebuild: make -C csrc bounds)")
+    print(r.stdout)                     # the checker's report (committed under profiles/ with -s)
     assert r.returncode == 0 and "violations 0" in r.stdout, (r.stdout, r.stderr[-3000:])
 
 
