@@ -16,12 +16,12 @@ import re
 import sqlite3
 from collections import defaultdict
 
-MANGLED = re.compile(r"gemm_kernel.*?Lb([01])ELb([01])E")
-DEMANGLED = re.compile(r"gemm_kernel<.*?(true|false), (true|false), jmt::TileCfg")
+MANGLED = re.compile(r"gemm_(?:persist3?_)?kernel.*?Lb([01])ELb([01])E")
+DEMANGLED = re.compile(r"gemm_(?:persist3?_)?kernel<.*?(true|false), (true|false), jmt::")
 
 
 def family(name: str):
-    if "gemm_kernel" in name:
+    if "gemm_kernel" in name or "gemm_persist" in name:
         m = MANGLED.search(name)
         if m:
             ak, bk = m.group(1) == "1", m.group(2) == "1"
@@ -46,6 +46,8 @@ def family(name: str):
         return "attn_fwd"
     if "attn_bwd_kernel" in name:
         return "attn_bwd"
+    if "attn_dkdv_kernel" in name:
+        return "attn_dkdv"
     return None
 
 
@@ -118,7 +120,8 @@ def main():
         rec = {"commit": os.environ.get("JMT_COMMIT"), "steps": steps,
                "ms_per_step": bench["ms_per_step"],
                "method": "rocprofv3 --kernel-trace over the default bench command; kernels of "
-                         "the last `steps` graph replays (the timed region, side stream on), "
+                         "the last `steps` graph replays (the timed region; the weight-gradient side "
+                         "stream as bench.py's default: off since round 4), "
                          "split-K reduce kernels added to their GEMM (scripts/family_from_trace.py)",
                "families": {}}
         for f in agg:
