@@ -20,8 +20,18 @@ MANGLED = re.compile(r"gemm_(?:persist3?_)?kernel.*?Lb([01])ELb([01])E")
 DEMANGLED = re.compile(r"gemm_(?:persist3?_)?kernel<.*?(true|false), (true|false), jmt::")
 
 
+# ROCm 7.2's demangler prints gemm_persist_kernel<__bf16, AK, BK, ...> as
+# "gemm_persist_kernel<bool _Accum, bool, E, BK, ..." — the A majorness is lost.  Every
+# persistent launch has a K-major A in practice (the weight gradients, A MN-major, are split-K,
+# which the persistent kernel does not take: gemm_persist.hip persist_choice), so BK decides.
+BROKEN_PERSIST = re.compile(r"gemm_persist3?_kernel<bool _Accum, bool, E, (true|false),")
+
+
 def family(name: str):
     if "gemm_kernel" in name or "gemm_persist" in name:
+        bp = BROKEN_PERSIST.search(name)
+        if bp:
+            return "gemm_NT" if bp.group(1) == "true" else "gemm_NN"
         m = MANGLED.search(name)
         if m:
             ak, bk = m.group(1) == "1", m.group(2) == "1"
