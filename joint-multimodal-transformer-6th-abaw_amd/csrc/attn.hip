@@ -324,20 +324,6 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
 // needs ~480 registers per wave (O 256 + Q 128 + working set) and spilled 256 VGPRs under hipcc:
 // not kept.  Phase stamps of this 16x16 kernel: profiles/r02_attn_phase_stamps.txt.)
 
-struct AttnBwdArgs {
-  const void* go;
-  const void* o;
-  const void* q;
-  const void* k;
-  const void* v;
-  const float* lse;
-  void* pbuf;
-  void* dsbuf;
-  void* dq;
-  int64_t sgo_l, sgo_n, so_l, so_n, sq_l, sq_n, sk_l, sk_n, sv_l, sv_n, sdq_l, sdq_n, ldp;
-  int Lq, Lk, H, nitems;
-  float scale, scale_log2;
-};
 
 // OPT: as attn_fwd_kernel (1 permlane reductions of Delta, 2 s_setprio(1) for waves 4-7, 4 the
 // next tile's K / V LDS-DMA issued in pieces between the score / dP MFMA batches); 16 each
@@ -774,7 +760,13 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
   a.nitems = ((Lq + AT_QT - 1) / AT_QT) * N * H;
   const dim3 grid(persistent_grid(a.nitems));
   hipStream_t st = as_stream(stream);
-  if (dt == JMT_BF16) {
+  static const int rg2 = [] {                     // 32 query rows per wave (attn_bwd2.hip)
+    const char* e = getenv("JMT_ATTN_BWD_RG2");
+    return e ? atoi(e) : 0;
+  }();
+  if (rg2) {
+    launch_attn_bwd_rg2(dt, grid, st, a);
+  } else if (dt == JMT_BF16) {
     switch (attn_opt_bwd()) {
       case 0: launch_bwd_bf16<0>(grid, st, a); break;
       case 16: launch_bwd_bf16<16>(grid, st, a); break;

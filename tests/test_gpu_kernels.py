@@ -544,6 +544,24 @@ def test_fused_attention_bwd_vs_fp32(cd, Lq, Lk, N):
     assert torch.isnan(dq[..., :E].float()).all() and torch.isnan(dq[..., 2 * E:].float()).all()
 
 
+def test_attn_bwd_rg2_bit_identical(tmp_path):
+    """JMT_ATTN_BWD_RG2=1 (csrc/attn_bwd2.hip: 4 waves, 32 query rows per wave) writes the same
+    P, dS and dQ bit for bit as the default 8-wave kernel (same per-row product order, same
+    canonical half-sum), at T = 300 / 1024, ragged 70 x 129 and Lk = 1 with more items than CUs."""
+    import subprocess
+    import sys
+    script = os.path.join(os.path.dirname(__file__), "_attn_rg2_eq.py")
+    f = str(tmp_path / "rg2.pt")
+    env = dict(os.environ, JMT_ATTN_BWD_RG2="0")
+    r = subprocess.run([sys.executable, script, "save", f], env=env, capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    env["JMT_ATTN_BWD_RG2"] = "1"
+    r = subprocess.run([sys.executable, script, "cmp", f], env=env, capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_gemm_splitk_fused_reduce_bit_identical(tmp_path):
     """JMT_SPLITK_FUSED=1 (the last split block of each tile reduces it, gemm.hip splitk_fixup)
     writes bit-identical outputs to the separate reduce launch; both run as child processes
