@@ -308,6 +308,9 @@ __device__ __forceinline__ void rowsum_store(const GemmParams& p, const GemmWork
   }
 }
 
+template <typename O, class C>
+__device__ __forceinline__ void splitk_fixup(const GemmParams& p, const GemmWork& wk);
+
 template <typename T, typename O, bool AK, bool BK, class C, bool RS = false>
 __global__ __launch_bounds__(C::NT, C::OCC)
 void gemm_kernel(GemmParams p) {
@@ -489,7 +492,18 @@ __device__ __forceinline__ void reduce_outputs(const GemmParams& p, int b, int m
   const float* src0 = p.ws + (int64_t)b * per + mn;
   int s = 0;
   if constexpr (W == 4) {
-    // four slab loads in flight per step, summed in split order
+    // eight (then four) slab loads in flight per step, summed in split order (the same sums as
+    // four at a time: bit-identical; no measurable change in the step, profiles/r04/
+    // splitk_reduce_depth_ab.txt)
+    for (; s + 8 <= p.splits; s += 8) {
+      float4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = *(const float4*)(src0 + (s + u) * sstride);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[0] += t[u].x; v[1] += t[u].y; v[2] += t[u].z; v[3] += t[u].w;
+      }
+    }
     for (; s + 4 <= p.splits; s += 4) {
       float4 t[4];
 #pragma unroll
