@@ -434,13 +434,18 @@ void gemm_kernel(GemmParams p) {
     // S-1 tiles in flight, one barrier per tile: the barrier of iteration kt also certifies that
     // every wave finished computing tile kt-1, whose buffer receives tile kt+S-1.
     static_assert(C::S <= 9 && (C::S - 2) * VMT < 64, "wait_tiles covers up to 7 newer tiles");
-    static_assert(C::BM * C::KB / 1024 % NWV == 0 && C::BN * C::KB / 1024 % NWV == 0,
-                  "an uneven LDS-DMA split needs the 2-stage pipeline");
+    // an uneven DMA split (the 160-row tile) deals a K-tile's instructions round-robin, so a
+    // wave's own count per K-tile depends on the wave: its waits count exactly those
+    constexpr bool EVEN = C::BM * C::KB / 1024 % NWV == 0 && C::BN * C::KB / 1024 % NWV == 0;
+    static_assert(EVEN || (C::S - 2) * VMT <= 16, "wait_vm covers up to 16");
+    const int cw = dma_count<C::BM * C::KB / 1024, NWV>(__builtin_amdgcn_readfirstlane(wid)) +
+                   dma_count<C::BN * C::KB / 1024, NWV>(__builtin_amdgcn_readfirstlane(wid));
 #pragma unroll
     for (int i = 0; i < C::S - 1; ++i)
       if (i < nfull) issue_ktile<T, AK, BK, C>(p, smem, cur, i, i);
     for (int kt = 0; kt < nfull; ++kt) {
-      wait_tiles<VMT>(min(C::S - 2, nfull - 1 - kt));
+      if constexpr (EVEN) wait_tiles<VMT>(min(C::S - 2, nfull - 1 - kt));
+      else wait_vm(min(C::S - 2, nfull - 1 - kt) * cw);
       __builtin_amdgcn_s_barrier();
       if (kt + C::S - 1 < nfull)
         issue_ktile<T, AK, BK, C>(p, smem, cur, kt + C::S - 1, (kt + C::S - 1) % C::S);
@@ -653,6 +658,10 @@ static void launch_layout(const GemmParams& p, int cfg, dim3 grid, hipStream_t s
     case 5: launch_cfg<T, O, AK, BK, Cfg5, RS>(p, grid, st); break;
     case 30: if constexpr (AK) { launch_cfg<T, O, AK, BK, Cfg30, RS>(p, grid, st); break; }
              [[fallthrough]];
+    case 31: if constexpr (AK && sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg31, RS>(p, grid, st); break; }
+             [[fallthrough]];
+    case 32: if constexpr (AK && sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg32, RS>(p, grid, st); break; }
+             [[fallthrough]];
     case 10: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg10, RS>(p, grid, st); break; }
              [[fallthrough]];
     case 11: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg11, RS>(p, grid, st); break; }
@@ -688,7 +697,7 @@ static void launch_t(const GemmParams& p, int ak, int bk, int cfg, dim3 grid, hi
 static void cfg_tile(int cfg, int& bm, int& bn) {
   switch (cfg) {
     case 5: case 20: bm = 256; bn = 256; break;
-    case 30: bm = 160; bn = 256; break;
+    case 30: case 31: case 32: bm = 160; bn = 256; break;
     default: bm = 128; bn = 128; break;
   }
 }
@@ -946,7 +955,7 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   if (cfg == 40 || cfg == 42) cfg = 5;      // persistent configs not applicable: same tiles
   if (cfg == 41) cfg = 20;
   if (dt == JMT_F32 && cfg >= 10) cfg = 1;   // occupancy configs: 16-bit only
-  if (cfg == 30 && !d->a_kmajor) cfg = 5;    // 160-row tile: K-major A only
+  if (cfg >= 30 && cfg <= 32 && !d->a_kmajor) cfg = 5;   // 160-row tiles: K-major A only
   if (!cfg) {
     int s_unused;
     plan(dt, d->M, d->N, d->K, batch0 * batch1, splits, cfg, s_unused);
@@ -961,6 +970,16 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   // 256x256 tile does not and runs the split-K qkv / FFN wgrad shapes at least as fast
   // (profiles/r03_wgrad_dbias.jsonl)
   if (d->n_dbias > 0 && cfg == 10) cfg = 5;
+  // the planner's 160x256 tile runs with 128-B K-tiles in 3 stages (Cfg32: two K-steps in flight;
+  // interleaved A/B 4.50 -> 4.46 ms/step, long-K single B*T-row GEMMs up to -5 %; 64-B K-tiles in
+  // 4 stages, Cfg31, lost 12-17 %: profiles/r04/gemm_tile160_stages.txt).  JMT_GEMM_TILE160=30 /
+  // 31 selects the others (A/B).
+  static const int t160 = [] {
+    const char* e = getenv("JMT_GEMM_TILE160");
+    const int v = e ? atoi(e) : 32;
+    return v >= 30 && v <= 32 ? v : 32;
+  }();
+  if (g_gemm_cfg == 0 && cfg == 30 && d->a_kmajor && dt != JMT_F32) cfg = t160;
   int bm, bn;
   cfg_tile(cfg, bm, bn);
   p.tiles_m = (d->M + bm - 1) / bm;

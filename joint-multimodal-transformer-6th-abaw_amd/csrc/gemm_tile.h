@@ -84,6 +84,11 @@ using Cfg21 = TileCfg<128, 128, 2, 2, 64, 4, 1, 1, 0, 2, 1>;
 // K-major A only (the MN-major image swizzle needs a power-of-two row count); the 20 A
 // instructions of a K-tile are dealt round-robin over the 8 waves (glds_tile, dma_count).
 using Cfg30 = TileCfg<160, 256, 2, 4, 128, 2, 1, 1, 0>;
+// the same tile with more K-steps in flight for the long-K single B*T-row GEMMs (hipBLASLt fills
+// its LDS ~1.8x faster per CU there): 64-B K-tiles in 4 stages (3 in flight, 106 KiB)
+// or 128-B K-tiles in 3 stages (2 in flight, 156 KiB); uneven DMA dealing, per-wave waits
+using Cfg31 = TileCfg<160, 256, 2, 4, 64, 4, 1, 1, 0>;
+using Cfg32 = TileCfg<160, 256, 2, 4, 128, 3, 1, 1, 0>;
 // (256x256 over 4 waves — 2x2, 128x128 each, 256 accumulators per lane in AGPRs, 64-B K-tiles,
 // 4 stages, one block / CU: the macro tile hipBLASLt picks on these shapes, profiles/
 // r02_hipblaslt_reference.txt — compiled without spills but measured 1.45-1.65x slower than

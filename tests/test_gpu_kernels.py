@@ -63,7 +63,7 @@ def test_gemm_layouts_dtypes(dt, ak, bk):
         assert torch.isnan(C[:, N:]).all(), "wrote outside N"
 
 
-@pytest.mark.parametrize("cfg", [1, 5, 10, 11, 20, 21, 30])
+@pytest.mark.parametrize("cfg", [1, 5, 10, 11, 20, 21, 30, 31, 32])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 def test_gemm_forced_configs(cfg, ak, bk):
     """Every tile configuration of the planner forced on every operand layout (bf16), on ragged
