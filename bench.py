@@ -171,14 +171,21 @@ class FamilyProbe:
         two = statistics.median(ms(b) for _, b in self.cal)
         over = max(0.0, one - (two - one))
         fam = {}
-        for f, fl, by, ev in self.rec:
+        # every probe step launches the same sequence: each launch position is timed by the
+        # median over the probe steps (one disturbed launch does not move its family), then
+        # summed per family as if each step had run at those medians
+        n = len(self.rec) // probe_steps if len(self.rec) % probe_steps == 0 else 0
+        med = [statistics.median(ms(self.rec[k * n + i][3]) for k in range(probe_steps))
+               for i in range(n)] if n else [ms(r[3]) for r in self.rec]
+        for i, (f, fl, by, ev) in enumerate(self.rec[:n] if n else self.rec):
             d = fam.setdefault(f, {"launches": 0, "ms": 0.0, "ms_raw": 0.0, "flops": 0.0,
                                    "bytes": 0.0})
-            d["launches"] += 1
-            d["ms_raw"] += ms(ev)
-            d["ms"] += max(ms(ev) - over, 1e-6)
-            d["flops"] += fl
-            d["bytes"] += by or 0.0
+            w = probe_steps if n else 1                # per-step medians stand for every step
+            d["launches"] += w
+            d["ms_raw"] += w * med[i]
+            d["ms"] += w * max(med[i] - over, 1e-6)
+            d["flops"] += w * fl
+            d["bytes"] += w * (by or 0.0)
         out = []
         for f, d in fam.items():
             tf = d["flops"] / (d["ms"] * 1e-3) / 1e12
@@ -554,7 +561,8 @@ def main():
                     "timed_over": f"{args.probe_steps} eager probe steps after the timed region "
                                   "(side stream off: each launch alone on the compute stream), "
                                   "one event pair per launch minus the empty-launch pair "
-                                  f"overhead ({psum['event_pair_overhead_us']} us)",
+                                  f"overhead ({psum['event_pair_overhead_us']} us), each "
+                                  "launch position at its median over the probe steps",
                     "families": psum["families"]}
     sfl = step_flops(B, T, **fl_kw)
     step_mfma = None
