@@ -8,8 +8,13 @@ vision_in_ft=2048) -> 2x losses.loss.CCCLoss(1) (global-batch statistics) -> bac
 all-reduce of the flat gradient (N>1) -> fused SGD-nesterov step (config_file.json:73-80).
 Random-init weights.  bf16 MFMA compute, fp32 master weights / statistics.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+    python bench.py [--gpus N] [--steps K] [--warmup W]      (N > 1: starts N ranks itself)
+    torchrun --nproc-per-node N bench.py --gpus N ...        (or one rank per GPU via torchrun)
+
+One process per GPU either way (RCCL).  The reference scales to every visible GPU by itself
+(main.py:487-491 wraps the model in DataParallel, tools.py:16-21); `--gpus N` without torchrun's
+environment makes this script the launcher: it starts N worker processes of itself before any
+GPU call, relays rank 0's JSON line and fails if any rank fails.
 
 Prints ONE JSON line (rank 0).  `value` = windows/s of the whole job (weak scaling: B=64 per GPU).
 """
@@ -293,9 +298,101 @@ def cpu_baseline(model_sd, fc_sd, audio, video, lv, la, steps=2):
                               "shared with the other GPU slots, so it is not used"}
 
 
+def launch_ranks(n: int, argv, script: str = None, backend: str = None) -> int:
+    """Start `n` worker processes of `script` (this file) with torchrun's environment (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT), one per GPU, and wait.
+    Called before anything touches the GPU (torch.cuda.device_count() does not initialise it on
+    ROCm), and the workers are children, never an exec of this process.  Rank 0's stdout lines
+    that are JSON objects are held back and printed on stdout once every rank has exited 0 (the
+    ONE bench line); every other line of every rank goes to stderr prefixed "[rank r]", as it
+    comes (the ranks' logs, and a sign of life for long runs).  Returns the exit status: 0 only
+    if every rank exited 0 and rank 0 printed a JSON line whose n_gpus is `n`; when one rank
+    fails the others are terminated (their own PIDs) after a grace period."""
+    import socket
+    import subprocess
+    import threading
+    backend = backend or os.environ.get("JMT_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and ndev < n:
+        print(f"bench.py --gpus {n}: only {ndev} GPU(s) visible; RCCL needs one rank per GPU "
+              "(JMT_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs)", file=sys.stderr)
+        return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = script or os.path.abspath(__file__)
+    procs, lines = [], []
+    lock = threading.Lock()
+
+    def pump(r, stream):
+        for line in stream:
+            if r == 0 and line.lstrip().startswith("{"):
+                with lock:
+                    lines.append(line.rstrip("\n"))
+                continue
+            sys.stderr.write(f"[rank {r}] {line}")
+            sys.stderr.flush()
+
+    threads = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), JMT_DIST_BACKEND=backend, JMT_LAUNCHER="bench.py")
+        p = subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env,
+                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                             bufsize=1)
+        procs.append(p)
+        t = threading.Thread(target=pump, args=(r, p.stdout), daemon=True)
+        t.start()
+        threads.append(t)
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = bad[0]
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    if failed is not None:
+        deadline = time.time() + 30.0
+        while time.time() < deadline and any(p.poll() is None for p in procs):
+            time.sleep(0.2)
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    for t in threads:
+        t.join(timeout=5)
+    if failed is not None:
+        print(f"bench.py --gpus {n}: rank {failed[0]} exited with status {failed[1]}",
+              file=sys.stderr)
+        return failed[1] if failed[1] > 0 else 1
+    if not lines:
+        print(f"bench.py --gpus {n}: rank 0 printed no JSON line", file=sys.stderr)
+        return 1
+    try:
+        got = json.loads(lines[-1]).get("n_gpus")
+    except ValueError:
+        got = None
+    if got != n:
+        print(f"bench.py --gpus {n}: rank 0 reported n_gpus={got}", file=sys.stderr)
+        return 1
+    print(lines[-1], flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without torchrun's environment and N > 1 this "
+                         "script starts them itself (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
@@ -335,6 +432,13 @@ def main():
     elif extra:
         ap.error(f"unrecognized arguments: {' '.join(extra)}")
 
+    if "WORLD_SIZE" not in os.environ:
+        if (args.gpus or 1) > 1:
+            # no torchrun around us: be the launcher (nothing has touched the GPU yet)
+            raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif args.gpus is not None and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus "
+                         f"{args.gpus}: one rank per GPU")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -467,11 +571,12 @@ def main():
 
     run = step
     graphed = None
-    # N > 1 captures the RCCL all-reduces (per bucket, on the communication stream) and the CCC
-    # statistics all-gather into the graph as well (tests/test_gpu_dist.py
-    # test_rccl_bucketed_step_sync_free_and_capturable): the eager step is host-bound (its issue
-    # time, host_issue_ms_per_eager_step, is about the GPU step time).  JMT_GRAPH_DIST=0 = eager.
-    use_graph = args.graph and (world == 1 or os.environ.get("JMT_GRAPH_DIST", "1") == "1")
+    # N > 1 runs the bucketed step eagerly: its host issue time (host_issue_ms_per_eager_step,
+    # ~3 ms at c3) is below the GPU step, and eager is the N > 1 path the GPU tests have run.
+    # JMT_GRAPH_DIST=1 captures the RCCL all-reduces (per bucket, on the communication stream)
+    # and the CCC all-gather into the step graph too (tests/test_gpu_dist.py
+    # test_rccl_bucketed_step_sync_free_and_capturable, world size 1 only).
+    use_graph = args.graph and (world == 1 or os.environ.get("JMT_GRAPH_DIST", "0") == "1")
     if use_graph:
         # the whole step as one hipGraph (jmt/graph.py): replay issues ~300 launches at once
         graphed = GraphedStep(step).capture(warmup=1)
@@ -572,7 +677,15 @@ def main():
                      "achieved_tflops": round(step_tf, 1),
                      "frac_of_peak": round(step_tf / (PEAK_BF16_TFLOPS * world), 4)}
 
+    if world > 1:
+        print(f"rank {rank}/{world}: cuda:{local} backend {backend}, {B} windows, "
+              f"{elapsed / args.steps * 1e3:.3f} ms/step (max over ranks), graph {use_graph}, "
+              f"final loss {last_loss:.6f}", file=sys.stderr, flush=True)
     parity = None
+    # the parity and CPU legs run on rank 0 alone: the CCC losses inside them must use local
+    # statistics (a loss group would all-gather with ranks that are not there)
+    group = jdist.loss_group()
+    jdist.set_loss_group(None)
     if rank == 0 and not args.no_parity:
         if (cfg["jm"], cfg["fmt"], cfg["fc"], k, heads, layers, Dv, Da) == \
                 ("TRANSFORMER", "FC", True, 1, 1, 1, 2048, 1024) and cd != torch.float32 and \
@@ -599,6 +712,7 @@ def main():
             jcfg is None:
         cpu = cpu_baseline(model_sd0, fc_sd0, audio, video, lv, la)
 
+    jdist.set_loss_group(group)
     if rank == 0:
         out = {
             "metric": "train windows/sec + CCC parity, B=64 T=300 A/V fusion, 1/2/4/8 MI355X",
@@ -623,6 +737,8 @@ def main():
             "cpu_baseline": cpu,
             "final_loss": round(last_loss, 6),
             "graph": bool(use_graph),
+            "launcher": (os.environ.get("JMT_LAUNCHER", "torchrun") if world > 1 else None),
+            "dist_backend": backend if world > 1 else None,
             "host_issue_ms_per_eager_step": round(host_issue_ms, 3),
         }
         print(json.dumps(out), flush=True)

@@ -282,7 +282,8 @@ __global__ __launch_bounds__(CT) void mask_indices_kernel(int64_t n, const float
 // np.digitize(y, linspace(lo, hi, k + 1)) - 1 with the top bin clamped (loss.py:44-48): the bin
 // is (number of edges <= y) - 1, edges in float64 as numpy builds them (i * step + lo, the last
 // = hi); NaN -> k - 1 (numpy gives len(edges)).  A label below lo gives bin -1, on which the
-// reference's F.cross_entropy raises: here it is counted (stats[2]) and the loss is NaN.
+// reference's F.cross_entropy raises: here it is counted (stats[2]), the loss is NaN and the
+// host side raises on the count (jmt/functional.py _ce_label_check).
 __device__ __forceinline__ int ce_bin(float yf, int k, float lo, float hi) {
   if (yf != yf) return k - 1;
   const double y = (double)yf, step = ((double)hi - (double)lo) / (double)k;

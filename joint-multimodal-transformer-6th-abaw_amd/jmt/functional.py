@@ -1112,20 +1112,20 @@ class CCCLossFn(Function):
             raise ValueError("ccc loss: `add` must be an fp32 scalar")
         ops.ccc_finish(kind, world, stats_all, bs, eps, loss, coef, add=add)
         ctx.save_for_backward(pred_c, lab, coef)
-        ctx.meta = (kind, k, ignore, lo, hi, pred.shape, add is not None)
+        ctx.meta = (kind, k, ignore, lo, hi, pred.shape, add.shape if add is not None else None)
         return loss
 
     @staticmethod
     def backward(ctx, g):
         pred, lab, coef = ctx.saved_tensors
-        kind, k, ignore, lo, hi, shape, has_add = ctx.meta
+        kind, k, ignore, lo, hi, shape, add_shape = ctx.meta
         g = g.to(torch.float32) if g.dtype != torch.float32 else g
         g = g.contiguous()
         dpred = torch.empty_like(pred)
         ops.ccc_bwd(kind, pred, lab, k, ignore, lo, hi, coef, g, dpred)
-        # d(add + loss) / d add = 1: the incoming gradient as is (no kernel)
+        # d(add + loss) / d add = 1: the incoming gradient as is (no kernel), in add's shape
         return (dpred.view(shape), None, None, None, None, None, None, None, None, None,
-                g if has_add else None)
+                g.view(add_shape) if add_shape is not None else None)
 
 
 def ccc_loss(pred, label, eps=1e-8, digitize_num=1, rng=(-1.0, 1.0), group=None, add=None):
@@ -1145,6 +1145,48 @@ def ccc_loss_ignore(pred, label, ignore=-5.0, group=None):
 
 
 _CE_EDGES: dict = {}
+_CE_PENDING: dict = {}       # device -> float64 count of out-of-range labels seen under capture
+# eager CELoss reads the out-of-range label count at once (one host read, where the reference's
+# own digitize synchronises); False defers it to the device flag like a captured step
+CE_EAGER_LABEL_CHECK = [True]
+
+
+def _ce_label_check(stats_all, dev):
+    """The reference digitizes on the host and F.cross_entropy raises IndexError on the bin -1
+    a label below range[0] gets (losses/loss.py:45-51).  The statistics kernel counts those
+    labels (stats[2] of every rank).  Eager: the count is read here (the reference synchronises
+    in the same place, y.data.cpu()) and a non-zero count raises.  Under hipGraph capture no host
+    read is possible: the count accumulates into a per-device flag on the device, which the next
+    eager CELoss call (or check_ce_labels()) reads and raises on."""
+    counts = stats_all[2::4]
+    capturing = dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
+    pend = _CE_PENDING.get(dev)
+    if pend is None:
+        if capturing:
+            raise RuntimeError("CELoss under graph capture: run it once eagerly first (the "
+                               "out-of-range label flag is allocated there)")
+        pend = _CE_PENDING[dev] = torch.zeros((), dtype=torch.float64, device=dev)
+    if capturing or not CE_EAGER_LABEL_CHECK[0]:
+        pend.add_(counts.sum())
+        return
+    check_ce_labels(dev, extra=counts)
+
+
+def check_ce_labels(dev=None, extra=None):
+    """Raise IndexError if a CELoss call since the last check saw a label below range[0] (the
+    count kept on the device while the step was replayed from a graph); clears the flag."""
+    devs = [dev] if dev is not None else list(_CE_PENDING)
+    bad = 0.0
+    for d in devs:
+        pend = _CE_PENDING.get(d)
+        if pend is not None:
+            bad += float(pend)
+            pend.zero_()
+    if extra is not None:
+        bad += float(extra.sum())
+    if bad > 0:
+        raise IndexError(f"CELoss: {int(bad)} label(s) below range[0] digitize to class -1 "
+                         "(Target -1 is out of bounds.)")
 
 
 class CELossFn(Function):
@@ -1191,6 +1233,7 @@ class CELossFn(Function):
         loss = torch.empty((), dtype=torch.float32, device=dev)
         coef = torch.empty(1, dtype=torch.float64, device=dev)
         ops.ce_finish(world, stats_all, loss, coef)
+        _ce_label_check(stats_all, dev)
         ctx.save_for_backward(xc, lab, coef, w)
         ctx.meta = (k, lo, hi, x.shape)
         return loss

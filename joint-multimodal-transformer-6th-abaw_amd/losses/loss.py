@@ -37,8 +37,11 @@ class CCCLoss(nn.Module):
 class CELoss(nn.Module):
     """loss.py:34-51: cross entropy against labels digitized into `digitize_num` bins
     (np.digitize over linspace(range, digitize_num + 1), top bin clamped) — digitize, weighted
-    log-softmax NLL and its gradient in HIP kernels (jmt_ce_*), no host round trip.  A label
-    below range[0] makes the reference raise in F.cross_entropy; here the loss is NaN."""
+    log-softmax NLL and its gradient in HIP kernels (jmt_ce_*).  A label below range[0] makes the
+    reference's F.cross_entropy raise IndexError (bin -1): the statistics kernel counts such
+    labels and the call raises IndexError too — at once when eager (one host read, where the
+    reference's host digitize synchronises), at the next eager call or
+    jmt.functional.check_ce_labels() when the step was replayed from a hipGraph."""
 
     def __init__(self, digitize_num, range=[-1, 1], weights=None):
         super(CELoss, self).__init__()

@@ -1,0 +1,108 @@
+"""bench.py as its own multi-rank launcher (the reference scales to every
+visible GPU by itself, main.py:487-491, tools.py:16-21): `python bench.py --gpus N` without
+torchrun's environment starts N ranks, relays rank 0's JSON line and fails if a rank fails.
+CPU tests drive the launcher with a stand-in worker (tests/_fake_rank.py) and the real bench.py
+up to its first GPU call; the GPU test runs the real 2-rank bench over gloo on one GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAKE = os.path.join(REPO, "tests", "_fake_rank.py")
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _bench():
+    sys.path.insert(0, REPO)
+    import bench
+    return bench
+
+
+def test_launcher_relays_rank0_json_and_rank_logs(capsys, monkeypatch):
+    b = _bench()
+    monkeypatch.delenv("FAKE_RANK_FAIL", raising=False)
+    monkeypatch.delenv("FAKE_RANK_NGPUS", raising=False)
+    rc = b.launch_ranks(3, ["--steps", "2"], script=FAKE, backend="gloo")
+    out, err = capsys.readouterr()
+    assert rc == 0
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1                                   # ONE JSON line on stdout
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 3 and j["launcher"] == "bench.py" and j["backend"] == "gloo"
+    for r in range(3):                                       # every rank's log, prefixed
+        assert f"[rank {r}] rank {r}/3 local {r} master 127.0.0.1:" in err
+    assert "['--steps', '2']" in err
+    assert "[rank 0] plain text on rank 0's stdout" in err
+
+
+@pytest.mark.parametrize("bad_rank", [0, 1])
+def test_launcher_fails_when_a_rank_fails(capsys, monkeypatch, bad_rank):
+    b = _bench()
+    monkeypatch.setenv("FAKE_RANK_FAIL", str(bad_rank))
+    rc = b.launch_ranks(2, [], script=FAKE, backend="gloo")
+    out, err = capsys.readouterr()
+    assert rc == 3
+    assert out.strip() == ""                                 # no bench line from a failed job
+    assert f"rank {bad_rank} exited with status 3" in err
+
+
+def test_launcher_rejects_wrong_n_gpus(capsys, monkeypatch):
+    b = _bench()
+    monkeypatch.delenv("FAKE_RANK_FAIL", raising=False)
+    monkeypatch.setenv("FAKE_RANK_NGPUS", "1")
+    rc = b.launch_ranks(2, [], script=FAKE, backend="gloo")
+    out, err = capsys.readouterr()
+    assert rc == 1 and out.strip() == "" and "n_gpus=1" in err
+
+
+def test_launcher_needs_one_gpu_per_rccl_rank(capsys):
+    b = _bench()
+    import torch
+    n = torch.cuda.device_count() + 1
+    assert b.launch_ranks(n, [], script=FAKE, backend="nccl") == 2
+    assert "RCCL needs one rank per GPU" in capsys.readouterr().err
+
+
+def _run_bench(args, env_extra, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, BENCH] + args, cwd=REPO, env=env, text=True,
+                          capture_output=True, timeout=timeout)
+
+
+def test_bench_world_size_must_match_gpus():
+    r = _run_bench(["--gpus", "4"], {"WORLD_SIZE": "2", "RANK": "0"}, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in r.stderr
+
+
+@pytest.mark.skipif(__import__("torch").cuda.is_available(), reason="CPU-only: ranks must fail")
+def test_bench_gpus2_on_cpu_box_launches_two_ranks_and_fails_loudly():
+    # the real bench.py: without a GPU both ranks fail at their first GPU call; the launcher
+    # shows both ranks' logs and exits non-zero with no bench line
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"],
+                   {"JMT_DIST_BACKEND": "gloo"})
+    assert r.returncode != 0
+    assert r.stdout.strip() == ""
+    assert "[rank 0]" in r.stderr and "[rank 1]" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_gloo_on_one_gpu():
+    """`python bench.py --gpus 2` (no torchrun): two gloo ranks on cuda:0 run the eager bucketed
+    step, rank 0 relays n_gpus 2 with parity passing, both ranks log."""
+    r = _run_bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "4",
+                    "--probe-steps", "1", "--no-cpu-baseline"],
+                   {"JMT_DIST_BACKEND": "gloo"}, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["launcher"] == "bench.py" and j["dist_backend"] == "gloo"
+    assert j["graph"] is False                               # N > 1 default: eager step
+    assert j["config"]["global_batch"] == 8
+    assert j["parity"]["pass"], j["parity"]
+    assert "[rank 0] rank 0/2" in r.stderr and "[rank 1] rank 1/2" in r.stderr
