@@ -262,6 +262,40 @@ def parity_check(model, fc, audio, video, lv, la, cd, jm, fmt, Dv, nwin=2, k=1, 
             "tolerance": 1e-2, "pass": bool(err <= 1e-2 and lerr <= 1e-2)}
 
 
+NORTH_STAR_TOL = {torch.float32: 1e-4, torch.bfloat16: 1e-2, torch.float16: 1e-2}
+
+
+def north_star_key(cd) -> str:
+    name = {torch.float32: "fp32", torch.bfloat16: "bf16", torch.float16: "fp16"}[cd]
+    return f"north_star_{name}_{NORTH_STAR_TOL[cd]:g}"
+
+
+def north_star_verdict(own: dict, cd, strict: dict = None) -> dict:
+    """BASELINE.json north_star: "logits/VA predictions that match the reference CPU path within
+    1e-4 fp32 / 1e-2 bf16 on fixed seeds".  The measure is the ABSOLUTE prediction error on the
+    bench's fixed-seed batch (windows 0-1, the bench model's weights after the timed steps) vs the
+    fp32 oracle; the spread-relative error of the discriminative check (conditioned weights whose
+    predictions spread O(1), every gradient under its own strict bound) is reported beside it
+    against the same number, as its own verdict."""
+    tol = NORTH_STAR_TOL[cd]
+    out = {"verdict": "pass" if own["pred_max_abs_err"] <= tol else "fail",
+           "measure": "max |pred_gpu - pred_oracle| over the V and A predictions (absolute), "
+                      "bench batch windows 0-1, fixed seeds, the bench model's weights",
+           "value": own["pred_max_abs_err"], "tolerance": tol,
+           "pred_abs_max": own["pred_abs_max"]}
+    if strict is not None and "pred_max_abs_err" in strict:
+        ab = strict["pred_max_abs_err"]
+        out["conditioned"] = {
+            "verdict": "pass" if ab <= tol else "fail", "value": ab, "tolerance": tol,
+            "measure": "the same absolute error on the windows of the strict window-subset "
+                       "check (conditioned hash-init weights, predictions spread O(0.1))",
+            "rel_to_spread": strict["pred_abs_err_rel_to_spread"],
+            "rounding_emulating_oracle_rel_to_spread": strict.get("pred_emulated_rel_to_spread"),
+            "note": "relative to the spread no bf16 path is within 1e-2 on these weights: the "
+                    "oracle with only its storage rounded to bf16 is at the value above"}
+    return out
+
+
 def cpu_threads():
     """Threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS, 16 per GPU on the
     GPU pool, whose nproc shows the whole machine) or the affinity set."""
@@ -704,9 +738,15 @@ def main():
             if args.parity_perturb:
                 parity["perturbed"] = ("cross_attention_v.out_proj.weight x %g on the GPU"
                                        % (1 + args.parity_perturb))
+            # north_star's own number on the bench's fixed-seed batch and its trained weights
+            own = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv,
+                               k=k, H=heads, L=layers)
+            parity["bench_weights"] = own
+            parity[north_star_key(cd)] = north_star_verdict(own, cd, parity)
         else:
             parity = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv,
                                   k=k, H=heads, L=layers)
+            parity[north_star_key(cd)] = north_star_verdict(parity, cd)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3" and \
             jcfg is None:

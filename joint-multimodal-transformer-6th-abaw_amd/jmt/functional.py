@@ -1094,7 +1094,9 @@ class CCCLossFn(Function):
         dev = pred.device
         pred_c = pred if pred.is_contiguous() else pred.contiguous()
         lab = label
-        if lab.dtype != torch.float32 or not lab.is_contiguous():
+        if lab.dtype == torch.float64:
+            lab = lab.float().contiguous()       # (the kernel's statistics are float64 anyway)
+        elif lab.dtype != torch.float32 or not lab.is_contiguous():
             lab = ops.cast(lab, torch.float32)
         stats = torch.empty(8, dtype=torch.float64, device=dev)
         ops.ccc_stats(kind, pred_c, lab, k, ignore, lo, hi, stats)

@@ -27,15 +27,15 @@ def main():
         tag, dt = case.split("/")
         gpu, emu = v["gpu"], v["emulated"]
         bnd = P.strict_bounds(emu, DT[dt])
-        margin = {k: (bnd[k] / gpu[k] if gpu[k] > 0 else math.inf) for k in emu}
-        ratio = [gpu[k] / emu[k] for k in emu if emu[k] > 0 and math.isfinite(gpu[k])]
+        margin = {k: (bnd[k] / gpu[k] if gpu[k] > 0 else math.inf) for k in bnd}
+        ratio = [gpu[k] / emu[k] for k in bnd if emu[k] > 0 and math.isfinite(gpu[k])]
         worst = sorted(margin, key=margin.get)[:5]
         print(json.dumps({
             "suite": "strict", "case": tag, "dtype": dt, "k_strict": P.K_STRICT,
-            "n_quantities": len(emu), "violations": sum(1 for k in emu if not gpu[k] <= bnd[k]),
+            "n_quantities": len(bnd), "violations": sum(1 for k in bnd if not gpu[k] <= bnd[k]),
             "min_margin": round(margin[worst[0]], 3),
-            "n_margin_below_1_5": sum(1 for k in emu if margin[k] < 1.5),
-            "min_margin_values": round(min(margin[k] for k in emu if P._is_value(k)), 3),
+            "n_margin_below_1_5": sum(1 for k in bnd if margin[k] < 1.5),
+            "min_margin_values": round(min(margin[k] for k in bnd if P._is_value(k)), 3),
             "worst": [{"q": k, "gpu": round(gpu[k], 6), "emulated": round(emu[k], 6),
                        "bound": round(bnd[k], 6), "margin": round(margin[k], 3)} for k in worst],
             "gpu_over_emulated": {"median": round(float(np.median(ratio)), 3),

@@ -35,8 +35,8 @@ def main():
             emu = P.emulated_strict(gold, c, cd)
             full["strict"][f"{c['tag']}/{str(cd)[6:]}"] = {"gpu": gpu, "emulated": emu}
             bnd = P.strict_bounds(emu, cd)
-            margin = {k: (bnd[k] / gpu[k] if gpu[k] > 0 else float("inf")) for k in gpu}
-            ratio = [gpu[k] / emu[k] for k in gpu if emu[k] > 0]
+            margin = {k: (bnd[k] / gpu[k] if gpu[k] > 0 else float("inf")) for k in bnd}
+            ratio = [gpu[k] / emu[k] for k in bnd if emu[k] > 0]
             worst = sorted(margin, key=margin.get)[:5]
             kinds = {}
             for k in gpu:
@@ -44,7 +44,8 @@ def main():
                 kinds.setdefault(kind, []).append(gpu[k])
             print(json.dumps({
                 "suite": "strict", "case": c["tag"], "dtype": str(cd)[6:],
-                "n_quantities": len(gpu), "violations": len(P.check16_strict(gpu, emu, cd)),
+                "n_quantities": len(bnd), "violations": len(P.check16_strict(gpu, emu, cd)),
+                "score_path_rows_bounded": sorted(k for k in bnd if k.endswith("[qk]")),
                 "min_margin": round(margin[worst[0]], 3),
                 "worst": [{"q": k, "gpu": round(gpu[k], 6), "emulated": round(emu[k], 6),
                            "bound": round(bnd[k], 6), "margin": round(margin[k], 3)}

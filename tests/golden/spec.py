@@ -32,9 +32,9 @@ TT_CASES = [
 # for fp32 and for the comparison with the reference's own 16-bit autocast path.
 COND_CASES = [
     dict(tag="cond_tr_fc", jm="TRANSFORMER", fmt="FC", H=1, L=1, B=4, T=61, vin=2048,
-         inter=True, gains=hi.GAINS_COND, loss="proj"),
+         inter=True, gains=hi.GAINS_COND, loss="proj", score_path=True),
     dict(tag="cond_tr_fc_t300", jm="TRANSFORMER", fmt="FC", H=1, L=1, B=2, T=300, vin=2048,
-         inter=True, gains=hi.GAINS_COND_T300, loss="proj"),
+         inter=True, gains=hi.GAINS_COND_T300, loss="proj", score_path=True),
     dict(tag="cond_none_fc", jm="NONE", fmt="FC", H=1, L=1, B=4, T=61, vin=2048, inter=True,
          gains=hi.GAINS_COND, loss="proj"),
     dict(tag="cond_tr_sa", jm="TRANSFORMER", fmt="SELF_ATTEN", H=1, L=1, B=2, T=37, vin=2048,

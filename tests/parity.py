@@ -195,7 +195,8 @@ def strict_errors(golden: dict, c: dict, vo, ao, l1, l2, grads, store) -> dict:
         q["out:" + k] = float(np.abs(a - b).max() / scale)
     for k, l in (("v_loss", l1), ("a_loss", l2)):
         q["out:" + k] = abs(float(l) - float(golden[f"{tag}/{k}"])) / scale
-    for k, e in grad_errors_rsample(golden, tag, grads).items():
+    for k, e in grad_errors_rsample(golden, tag, grads,
+                                    score_path=bool(c.get("score_path"))).items():
         # the inputs' gradients are activation gradients (ceiling of the intermediates)
         q[("inter:" if k.startswith("input.") else "param:") + k] = e
     if c.get("inter"):
@@ -259,17 +260,26 @@ def _is_value(q: str) -> bool:
     return q.startswith("out:") or q.endswith(":val")
 
 
+def score_path_bounded(k: str, e_emu: float, cd) -> bool:
+    """The Q / K rows of an in_proj gradient (`name[qk]`, cases with score_path) enter the strict
+    suite where the rounding-emulating oracle's own error is at most half the ceiling, so that
+    the bound min(ceiling, K_STRICT x emulated) leaves at least 2x the emulation: where attention
+    is flat or saturated the emulation alone is O(10-60 %) off in bf16 (the case's conditioning,
+    not the implementation; profiles/r03_parity_conditioning.txt) and no 16-bit bound applies."""
+    return not k.endswith("[qk]") or e_emu <= 0.5 * CEIL[cd][k.split(":")[0]]
+
+
 def strict_bounds(emu: dict, cd) -> dict:
     u = UNIT[cd]
     return {k: min(CEIL[cd][k.split(":")[0]], K_STRICT * max(e, (0.5 if _is_value(k) else 2.0) * u))
-            for k, e in emu.items()}
+            for k, e in emu.items() if score_path_bounded(k, e, cd)}
 
 
 def check16_strict(gpu: dict, emu: dict, cd) -> list:
     """-> list of (quantity, gpu_err, bound) breaking the strict bounds (a zero reference
     gradient — an unused parameter — must be exactly zero: grad_errors gives 0 or inf)."""
     b = strict_bounds(emu, cd)
-    return [(k, gpu[k], b[k]) for k in emu if not (gpu[k] <= b[k])]
+    return [(k, gpu[k], b[k]) for k in b if not (gpu[k] <= b[k])]
 
 
 # ---- comparison with the reference's own 16-bit path (spec.TT_CASES) -------------------------
@@ -433,6 +443,11 @@ def window_subset_check(cd=torch.bfloat16, B: int = 64, T: int = 300, win=(0, 21
             "pred_err_max_rel_to_largest": round(max(r[1] for r in pred), 5),
             "pred_bound": round(min(r[2] for r in pred), 5),
             "pred_abs_err_rel_to_spread": round(pred_abs / spread, 5),
+            "pred_max_abs_err": float(f"{pred_abs:.3g}"),
+            "pred_emulated_rel_to_largest": round(max(
+                float((evo - rvo).abs().max()), float((eao - rao).abs().max())) / mx, 5),
+            "pred_emulated_rel_to_spread": round(max(
+                float((evo - rvo).abs().max()), float((eao - rao).abs().max())) / spread, 5),
             "out_layer1_grad_rel_err": round(ol1[0][1], 5) if ol1 else None,
             "out_layer1_grad_bound": round(ol1[0][2], 5) if ol1 else None,
             "loss_abs_err_vs_oracle_ccc": float(f"{loss_err:.3g}"),
