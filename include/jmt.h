@@ -23,7 +23,9 @@
 extern "C" {
 #endif
 
-#define JMT_ABI_VERSION 5
+#define JMT_ABI_VERSION 6
+/* ABI 6 (round 5): jmt_attn_bwd_km removed (the key-major P / dS hand-off measured slower than
+ * jmt_attn_bwd + jmt_attn_dkdv); the split-K workspace holds the fp32 slabs only. */
 
 enum { JMT_F32 = 0, JMT_BF16 = 1, JMT_F16 = 2 };
 enum { JMT_OK = 0, JMT_ERR_ARG = -1, JMT_ERR_HIP = -2, JMT_ERR_UNSUPPORTED = -3 };
@@ -202,17 +204,6 @@ int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* go, i
                  const void* v, int64_t sv_l, int64_t sv_n, const float* lse, void* p_out,
                  void* ds_out, int64_t ldp, void* dq, int64_t sdq_l, int64_t sdq_n, float scale,
                  void* stream);
-
-/* jmt_attn_bwd with P and dS handed over KEY-major (round 3): p_out / ds_out row
- * (n*H + h)*Lk + k holds key k's probabilities / dS over the queries (columns [0, Lq), row stride
- * ldt >= Lq, columns [Lq, ldt) not written), so the dK = ds^T Q and dV = P^T dO products read a
- * K-major A operand (jmt_gemm's 160 x 256 tile applies); dq as jmt_attn_bwd. */
-int jmt_attn_bwd_km(int dt, int N, int H, int Lq, int Lk, int dh, const void* go, int64_t sgo_l,
-                    int64_t sgo_n, const void* o, int64_t so_l, int64_t so_n, const void* q,
-                    int64_t sq_l, int64_t sq_n, const void* k, int64_t sk_l, int64_t sk_n,
-                    const void* v, int64_t sv_l, int64_t sv_n, const float* lse, void* p_out,
-                    void* ds_out, int64_t ldt, void* dq, int64_t sdq_l, int64_t sdq_n,
-                    float scale, void* stream);
 
 /* Key-side attention gradients from the handed-over probabilities (round 4): per (n, h)
  * dV = P^T dO and dK = dS^T Q, P / dS as jmt_attn_bwd writes them (row (n*H + h)*Lq + q, keys in

@@ -77,7 +77,7 @@ __device__ __forceinline__ void stamp(uint64_t* buf, int idx) {
   }
 }
 
-// OPT (development A/B switch, JMT_ATTN_OPT; bits): 1 lane-group reductions by permlane swaps
+// OPT (compile-time schedule bits, ATTN_FWD_OPT below): 1 lane-group reductions by permlane swaps
 // instead of ds_bpermute shuffles; 2 s_setprio(1) for the second-dispatched half (waves 4-7, the
 // arbitration loser of every phase: MI355X_MICROARCH "Two waves per SIMD" item 4); 4 the next
 // K tile's LDS-DMA issued in pieces between the P V MFMA batches instead of in one burst after
@@ -330,9 +330,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_kernel(AttnFwdArgs p) {
 // tile's P / dS row stores deferred to the start of the next tile: the end-of-tile
 // vmcnt(0) that waits for the next tile's DMA otherwise also waits for the acknowledgement of
 // the stores issued just before it (stores count in vmcnt, in issue order)
-// KM: P and dS handed over KEY-major (rows (n H + h) Lk + key, query columns, stride ldp >= Lq) so
-// that dK = (dS^T) Q and dV = (P^T) dO read a K-major A operand (jmt_attn_bwd_km)
-template <typename T, int OPT = 0, bool KM = false>
+template <typename T, int OPT = 0>
 __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
   typedef typename Frag16<T>::t F;
   typedef typename Frag16<T>::h Hf;
@@ -534,14 +532,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
         }
         const int key = kbase + 16 * kt;
         JMT_DCHECK(qc >= 0 && qc < p.Lq && item < p.nitems);
-        if constexpr (KM) {                         // 2-B stores down the key rows
-          if (qr < p.Lq) {
-            T* col = (T*)(h == 0 ? p.pbuf : p.dsbuf) + (int64_t)nh * p.Lk * p.ldp + qr;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (key + r < p.Lk) col[(int64_t)(key + r) * p.ldp] = h == 0 ? pv4[r] : ds4[r];
-          }
-        } else if constexpr ((OPT & 16) != 0) {
+        if constexpr ((OPT & 16) != 0) {
           pend[kt] = h == 0 ? *(const uint2*)pv4 : *(const uint2*)ds4;
           pend_key[kt] = key;
         } else if (qr < p.Lq && key < p.ldp) {
@@ -549,7 +540,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
           else *(uint2*)(prow_ds + key) = *(const uint2*)ds4;
         }
       }
-      if constexpr ((OPT & 16) != 0 && !KM) pend_on = true;
+      if constexpr ((OPT & 16) != 0) pend_on = true;
       // ---- acc[t] += sum_k dS(k) K[k][256h + 16t + 4g + r] (transposed K fragments in
       // double-buffered batches of 4)
       {
@@ -620,23 +611,15 @@ static int check_common(const char* name, int N, int H, int Lq, int Lk, const vo
 
 using namespace jmt;
 
-static void* g_stamps = nullptr;
+[[maybe_unused]] static void* g_stamps = nullptr;
 
-// JMT_ATTN_OPT (development A/B switch, read once): the OPT bits of the bf16 kernels (forward:
-// bits 1, 2, 4, 8; backward: 1, 2, 4, 16).  Defaults = the measured-fastest combination
-// (profiles/r03_attn_opt_ab.jsonl, interleaved A/B at the c3 launches: forward 1|2|8, backward
-// 1|2|4; the fp16 kernels use the same).
+// Schedule options of the bf16 / fp16 kernels (OPT bits, compile time; forward: 1 permlane
+// reductions, 2 setprio for waves 4-7, 4 interleaved K-tile DMA, 8 split exponentials;
+// backward: 1, 2, 4, 16 deferred P / dS stores).  The measured-fastest combination is the only
+// one compiled (profiles/r03_attn_opt_ab.jsonl, interleaved A/B at the c3 launches: forward
+// 1|2|8, backward 1|2|4).
 constexpr int ATTN_FWD_OPT = 11;
 constexpr int ATTN_BWD_OPT = 7;
-static int attn_opt_env() {
-  static int v = [] {
-    const char* e = getenv("JMT_ATTN_OPT");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
-}
-static int attn_opt_fwd() { return attn_opt_env() < 0 ? ATTN_FWD_OPT : (attn_opt_env() & 15); }
-static int attn_opt_bwd() { return attn_opt_env() < 0 ? ATTN_BWD_OPT : (attn_opt_env() & 23); }
 
 template <int OPT>
 static void launch_fwd_bf16(dim3 grid, hipStream_t st, const AttnFwdArgs& a) {
@@ -650,13 +633,6 @@ static void launch_bwd_bf16(dim3 grid, hipStream_t st, const AttnBwdArgs& a) {
   static bool once = (set_lds(attn_bwd_kernel<__bf16, OPT>, AB_LDS), true);
   (void)once;
   hipLaunchKernelGGL((attn_bwd_kernel<__bf16, OPT>), grid, dim3(512), (size_t)AB_LDS, st, a);
-}
-template <typename T>
-static void launch_bwd_km(dim3 grid, hipStream_t st, const AttnBwdArgs& a) {
-  constexpr int O = ATTN_BWD_OPT & ~16;
-  static bool once = (set_lds(attn_bwd_kernel<T, O, true>, AB_LDS), true);
-  (void)once;
-  hipLaunchKernelGGL((attn_bwd_kernel<T, O, true>), grid, dim3(512), (size_t)AB_LDS, st, a);
 }
 
 // one block per CU (the 160 KiB of LDS admit one), rounded down to a multiple of 8 (XCDs), when
@@ -676,10 +652,16 @@ static unsigned persistent_grid(int nitems) {
 }
 
 // diagnostic: route jmt_attn_fwd (bf16) through the phase-stamped kernel, stamps into `buf`
-// (2 x 256 x 64 uint64); NULL turns it off.  Not part of include/jmt.h (dev tool).
+// (2 x 256 x 64 uint64); NULL turns it off.  Only in the diagnostic build (make diag,
+// -DJMT_DIAG=1); not part of include/jmt.h (dev tool).
 extern "C" int jmt_attn_set_stamps(void* buf) {
+#if JMT_DIAG
   g_stamps = buf;
   return JMT_OK;
+#else
+  return buf ? set_error(JMT_ERR_UNSUPPORTED, "jmt_attn_set_stamps: diagnostic build only "
+                                              "(make diag)") : JMT_OK;
+#endif
 }
 
 extern "C" int jmt_attn_supported(int dt, int dh) {
@@ -707,20 +689,19 @@ extern "C" int jmt_attn_fwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
   hipStream_t st = as_stream(stream);
   a.nitems = ((Lq + AT_QT - 1) / AT_QT) * N * H;
   const dim3 grid(persistent_grid(a.nitems));
+#if JMT_DIAG
   if (g_stamps && dt == JMT_BF16) {   // diagnostic: phase stamps (jmt_attn_set_stamps)
     a.stamps = (uint64_t*)g_stamps;
-    static bool once = (set_lds(attn_fwd_kernel<__bf16, true>, AF_LDS), true);
+    static bool once = (set_lds(attn_fwd_kernel<__bf16, true, ATTN_FWD_OPT>, AF_LDS), true);
     (void)once;
-    hipLaunchKernelGGL((attn_fwd_kernel<__bf16, true>), grid, dim3(512), (size_t)AF_LDS, st, a);
-  } else if (dt == JMT_BF16) {
-    switch (attn_opt_fwd()) {
-      case 0: launch_fwd_bf16<0>(grid, st, a); break;
-      case 1: launch_fwd_bf16<1>(grid, st, a); break;
-      case 2: launch_fwd_bf16<2>(grid, st, a); break;
-      case 4: launch_fwd_bf16<4>(grid, st, a); break;
-      case 8: launch_fwd_bf16<8>(grid, st, a); break;
-      default: launch_fwd_bf16<ATTN_FWD_OPT>(grid, st, a); break;
-    }
+    hipLaunchKernelGGL((attn_fwd_kernel<__bf16, true, ATTN_FWD_OPT>), grid, dim3(512),
+                       (size_t)AF_LDS, st, a);
+    JMT_LAUNCH_CHECK("jmt_attn_fwd");
+    return JMT_OK;
+  }
+#endif
+  if (dt == JMT_BF16) {
+    launch_fwd_bf16<ATTN_FWD_OPT>(grid, st, a);
   } else {
     static bool once = (set_lds(attn_fwd_kernel<_Float16, false, ATTN_FWD_OPT>, AF_LDS), true);
     (void)once;
@@ -760,19 +741,8 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
   a.nitems = ((Lq + AT_QT - 1) / AT_QT) * N * H;
   const dim3 grid(persistent_grid(a.nitems));
   hipStream_t st = as_stream(stream);
-  static const int rg2 = [] {                     // 32 query rows per wave (attn_bwd2.hip)
-    const char* e = getenv("JMT_ATTN_BWD_RG2");
-    return e ? atoi(e) : 0;
-  }();
-  if (rg2) {
-    launch_attn_bwd_rg2(dt, grid, st, a);
-  } else if (dt == JMT_BF16) {
-    switch (attn_opt_bwd()) {
-      case 0: launch_bwd_bf16<0>(grid, st, a); break;
-      case 16: launch_bwd_bf16<16>(grid, st, a); break;
-      case 23: launch_bwd_bf16<23>(grid, st, a); break;
-      default: launch_bwd_bf16<ATTN_BWD_OPT>(grid, st, a); break;
-    }
+  if (dt == JMT_BF16) {
+    launch_bwd_bf16<ATTN_BWD_OPT>(grid, st, a);
   } else {
     static bool once = (set_lds(attn_bwd_kernel<_Float16, ATTN_BWD_OPT>, AB_LDS), true);
     (void)once;
@@ -783,39 +753,3 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
   return JMT_OK;
 }
 
-// P / dS handed over key-major: p_out / ds_out rows (n*H + h)*Lk + key, columns = queries, row
-// stride ldt >= Lq (include/jmt.h); everything else as jmt_attn_bwd
-extern "C" int jmt_attn_bwd_km(int dt, int N, int H, int Lq, int Lk, int dh, const void* go,
-                               int64_t sgo_l, int64_t sgo_n, const void* o, int64_t so_l,
-                               int64_t so_n, const void* q, int64_t sq_l, int64_t sq_n,
-                               const void* k, int64_t sk_l, int64_t sk_n, const void* v,
-                               int64_t sv_l, int64_t sv_n, const float* lse, void* p_out,
-                               void* ds_out, int64_t ldt, void* dq, int64_t sdq_l, int64_t sdq_n,
-                               float scale, void* stream) {
-  if (N == 0 || Lq == 0) return JMT_OK;
-  if (!jmt_attn_supported(dt, dh))
-    return set_error(JMT_ERR_UNSUPPORTED, "jmt_attn_bwd_km: dtype %d / head dim %d not supported",
-                     dt, dh);
-  const void* ptrs[] = {go, o, q, k, v, p_out, ds_out, dq};
-  const int64_t strides[] = {sgo_l, sgo_n, so_l, so_n, sq_l, sq_n, sk_l, sk_n, sv_l, sv_n,
-                             sdq_l, sdq_n, ldt};
-  int rc = check_common("jmt_attn_bwd_km", N, H, Lq, Lk, ptrs, 8, strides, 13);
-  if (rc != JMT_OK) return rc;
-  JMT_CHECK_ARG(lse && ldt >= Lq, "jmt_attn_bwd_km: lse missing or ldt < Lq");
-  AttnBwdArgs a = {};
-  a.go = go; a.o = o; a.q = q; a.k = k; a.v = v; a.lse = lse;
-  a.pbuf = p_out; a.dsbuf = ds_out; a.dq = dq;
-  a.sgo_l = sgo_l; a.sgo_n = sgo_n; a.so_l = so_l; a.so_n = so_n; a.sq_l = sq_l; a.sq_n = sq_n;
-  a.sk_l = sk_l; a.sk_n = sk_n; a.sv_l = sv_l; a.sv_n = sv_n; a.sdq_l = sdq_l; a.sdq_n = sdq_n;
-  a.ldp = ldt;
-  a.Lq = Lq; a.Lk = Lk; a.H = H;
-  a.scale = scale;
-  a.scale_log2 = scale * 1.4426950408889634f;
-  a.nitems = ((Lq + AT_QT - 1) / AT_QT) * N * H;
-  const dim3 grid(persistent_grid(a.nitems));
-  hipStream_t st = as_stream(stream);
-  if (dt == JMT_BF16) launch_bwd_km<__bf16>(grid, st, a);
-  else launch_bwd_km<_Float16>(grid, st, a);
-  JMT_LAUNCH_CHECK("jmt_attn_bwd_km");
-  return JMT_OK;
-}

@@ -9,7 +9,7 @@ namespace jmt {
 constexpr int AT_DH = 512;          // head dim of the fused kernels
 constexpr int AT_ROWB = 1024;       // bytes per image row (DH 16-bit values)
 
-// arguments of the long-sequence attention backward (attn.hip attn_bwd_kernel, attn_bwd2.hip)
+// arguments of the long-sequence attention backward (attn.hip attn_bwd_kernel)
 struct AttnBwdArgs {
   const void* go;
   const void* o;
@@ -24,10 +24,6 @@ struct AttnBwdArgs {
   int Lq, Lk, H, nitems;
   float scale, scale_log2;
 };
-
-// attn_bwd2.hip: the backward with 32 query rows per wave (4 waves, one per SIMD); dt = JMT_BF16
-// or JMT_F16
-void launch_attn_bwd_rg2(int dt, dim3 grid, hipStream_t st, const AttnBwdArgs& a);
 
 // byte offset of logical byte b of row `row` in a swizzled image
 __device__ __forceinline__ int img_off(int row, int b) {

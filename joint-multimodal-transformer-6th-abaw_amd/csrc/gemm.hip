@@ -308,9 +308,6 @@ __device__ __forceinline__ void rowsum_store(const GemmParams& p, const GemmWork
   }
 }
 
-template <typename O, class C>
-__device__ __forceinline__ void splitk_fixup(const GemmParams& p, const GemmWork& wk);
-
 template <typename T, typename O, bool AK, bool BK, class C, bool RS = false>
 __global__ __launch_bounds__(C::NT, C::OCC)
 void gemm_kernel(GemmParams p) {
@@ -474,10 +471,6 @@ void gemm_kernel(GemmParams p) {
   trace_stamp(p, 2);
   gemm_epilogue<T, O, C>(p, cur, acc, lane, wm, wn);
   if constexpr (RS) rowsum_store<C>(p, cur, rsum, lane, wm);
-  if (p.splits > 1 && p.counters) {
-    if (p.c_dtype == JMT_F32) splitk_fixup<float, C>(p, cur);
-    else splitk_fixup<T, C>(p, cur);
-  }
   trace_stamp(p, 3);
 }
 
@@ -575,52 +568,11 @@ __device__ __forceinline__ void reduce_outputs(const GemmParams& p, int b, int m
   }
 }
 
-// split-K inside the launch: after writing its partial slab, each split block of an output tile
-// takes a ticket on the tile's counter; the block that draws the last one reduces the tile
-// (reduce_outputs, split order: the bits of splitk_reduce_kernel).  Publication per
-// cdna_hip_programming.md §5 'Projection GEMM at M = 256' item 2 / Guideline 16: every wave
-// drains its slab stores (vmcnt(0)), a block barrier, lane 0's agent-scope release, vmcnt(0)
-// (hipcc may drop the fence's own), the relaxed agent fetch_add; the last arriver's lane 0 does
-// the agent-scope acquire + vmcnt(0) before a barrier and the slab loads.  Any placement of a
-// tile's splits over CUs / XCDs is correct; the counters are zeroed by a memset node ahead of
-// the launch.  Replaces a separate reduce launch that ran 10-90 us per weight gradient in the
-// step (profiles/r04/step_trace_g8.txt).
-template <typename O, class C>
-__device__ __forceinline__ void splitk_fixup(const GemmParams& p, const GemmWork& wk) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  volatile int* flag = (volatile int*)smem;
-  if (threadIdx.x == 0) {
-    const int tile = (wk.b * p.tiles_m + wk.m0 / C::BM) * p.tiles_n + wk.n0 / C::BN;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int prev = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == p.splits - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  const bool v4 = p.N % 4 == 0 && p.c_vec4;
-  const int mrows = min(C::BM, p.M - wk.m0), ncols = min(C::BN, p.N - wk.n0);
-  if (v4) {
-    const int nq = ncols / 4;                          // ncols % 4 == 0 (N, n0 multiples of 4)
-    for (int e = threadIdx.x; e < mrows * nq; e += C::NT) {
-      const int r = e / nq, q = e - r * nq;
-      reduce_outputs<O, 4>(p, wk.b, wk.m0 + r, wk.n0 + 4 * q);
-    }
-  } else {
-    for (int e = threadIdx.x; e < mrows * ncols; e += C::NT) {
-      const int r = e / ncols, q = e - r * ncols;
-      reduce_outputs<O, 1>(p, wk.b, wk.m0 + r, wk.n0 + q);
-    }
-  }
-}
+// (split-K reduced inside the GEMM launch by each tile's last-arriving split block — agent-scope
+// release / acquire on a per-tile counter, bit-identical to the separate launch — measured slower:
+// every tile of a weight gradient finishes in the last wave, so the fused reductions ran on one
+// CU per tile at the end of the launch, TN b3 512x512x19200 58 -> 93 us, the step 4.65 -> 5.43 ms;
+// profiles/r04/splitk_fused_ab.txt.  Removed in round 5.)
 
 // split-K reduction + epilogue.  Vector form (N % 4 == 0, C 4-element aligned): one thread per 4
 // consecutive outputs, float4 slab loads; otherwise one thread per output element.
@@ -656,10 +608,6 @@ template <typename T, typename O, bool AK, bool BK, bool RS = false>
 static void launch_layout(const GemmParams& p, int cfg, dim3 grid, hipStream_t st) {
   switch (cfg) {
     case 5: launch_cfg<T, O, AK, BK, Cfg5, RS>(p, grid, st); break;
-    case 30: if constexpr (AK) { launch_cfg<T, O, AK, BK, Cfg30, RS>(p, grid, st); break; }
-             [[fallthrough]];
-    case 31: if constexpr (AK && sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg31, RS>(p, grid, st); break; }
-             [[fallthrough]];
     case 32: if constexpr (AK && sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg32, RS>(p, grid, st); break; }
              [[fallthrough]];
     case 10: if constexpr (sizeof(T) == 2) { launch_cfg<T, O, AK, BK, Cfg10, RS>(p, grid, st); break; }
@@ -697,7 +645,7 @@ static void launch_t(const GemmParams& p, int ak, int bk, int cfg, dim3 grid, hi
 static void cfg_tile(int cfg, int& bm, int& bn) {
   switch (cfg) {
     case 5: case 20: bm = 256; bn = 256; break;
-    case 30: case 31: case 32: bm = 160; bn = 256; break;
+    case 32: bm = 160; bn = 256; break;
     default: bm = 128; bn = 128; break;
   }
 }
@@ -751,10 +699,10 @@ static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, in
   // 81: profiles/r03_c2_gemm_tiles.jsonl), so they are keyed to >= 16,384 rows.
   if (splits <= 1 && ak && M >= 16384 && K >= 512 && K % 64 == 0 &&
       ((batch == 1 && N <= 1024) || (bk && batch == 3 && N == 1536 && K == 512)))
-    return 30;
+    return 32;
   // the stacked-stream dgrad of out_layer_pv (b2, beta = 1): 65 -> 57 us (1.17 waves of 256x256
   // tiles, 1.88 of 160x256; profiles/r03_nn_sweep.jsonl)
-  if (splits <= 1 && ak && !bk && batch == 2 && M >= 4096 && N == 512 && K == 512) return 30;
+  if (splits <= 1 && ak && !bk && batch == 2 && M >= 4096 && N == 512 && K == 512) return 32;
   if (!ak && !bk && M >= 1536 && N >= 512 && batch >= 3 && K >= 16384)
     return 10;                                                   // split-K qkv wgrad
   if (!ak && !bk && batch == 6 && M == 1024 && N == 512 && K >= 8192)
@@ -820,19 +768,10 @@ extern "C" int jmt_gemm_plan_splits(int ab_dtype, int M, int N, int K, int batch
   return splits;
 }
 
-// split-K workspace: the fp32 partial slabs, then one arrival counter per (batch, output tile)
-// for the in-launch reduction (sized for the smallest tile, 128 x 128)
-static size_t splitk_slab_bytes(int M, int N, int batch, int splits) {
-  return (size_t)splits * (size_t)batch * (size_t)M * (size_t)N * sizeof(float);
-}
-static size_t splitk_counter_bytes(int M, int N, int batch) {
-  const size_t n = (size_t)((M + 127) / 128) * (size_t)((N + 127) / 128) * (size_t)batch;
-  return (n * sizeof(int) + 255) / 256 * 256;
-}
-
+// split-K workspace: the fp32 partial slabs
 extern "C" size_t jmt_gemm_workspace_bytes(int M, int N, int batch, int splits) {
   if (splits <= 1) return 0;
-  return splitk_slab_bytes(M, N, batch, splits) + splitk_counter_bytes(M, N, batch);
+  return (size_t)splits * (size_t)batch * (size_t)M * (size_t)N * sizeof(float);
 }
 
 extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
@@ -952,10 +891,9 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
       return JMT_OK;
     }
   }
-  if (cfg == 40 || cfg == 42) cfg = 5;      // persistent configs not applicable: same tiles
-  if (cfg == 41) cfg = 20;
-  if (dt == JMT_F32 && cfg >= 10) cfg = 1;   // occupancy configs: 16-bit only
-  if (cfg >= 30 && cfg <= 32 && !d->a_kmajor) cfg = 5;   // 160-row tiles: K-major A only
+  if (cfg == 40) cfg = 5;                   // persistent config not applicable: same tile
+  if (dt == JMT_F32 && cfg >= 10) cfg = 1;   // occupancy / 160-row configs: 16-bit only
+  if (cfg == 32 && !d->a_kmajor) cfg = 5;    // 160-row tile: K-major A only
   if (!cfg) {
     int s_unused;
     plan(dt, d->M, d->N, d->K, batch0 * batch1, splits, cfg, s_unused);
@@ -970,45 +908,17 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   // 256x256 tile does not and runs the split-K qkv / FFN wgrad shapes at least as fast
   // (profiles/r03_wgrad_dbias.jsonl)
   if (d->n_dbias > 0 && cfg == 10) cfg = 5;
-  // the planner's 160x256 tile runs with 128-B K-tiles in 3 stages (Cfg32: two K-steps in flight;
-  // interleaved A/B 4.50 -> 4.46 ms/step, long-K single B*T-row GEMMs up to -5 %; 64-B K-tiles in
-  // 4 stages, Cfg31, lost 12-17 %: profiles/r04/gemm_tile160_stages.txt).  JMT_GEMM_TILE160=30 /
-  // 31 selects the others (A/B).
-  static const int t160 = [] {
-    const char* e = getenv("JMT_GEMM_TILE160");
-    const int v = e ? atoi(e) : 32;
-    return v >= 30 && v <= 32 ? v : 32;
-  }();
-  if (g_gemm_cfg == 0 && cfg == 30 && d->a_kmajor && dt != JMT_F32) cfg = t160;
   int bm, bn;
   cfg_tile(cfg, bm, bn);
   p.tiles_m = (d->M + bm - 1) / bm;
   p.tiles_n = (d->N + bn - 1) / bn;
   hipStream_t st = as_stream(stream);
-  // JMT_SPLITK_FUSED=1: split-K reduced by the last-arriving split block of each tile
-  // (splitk_fixup, bit-identical to the separate reduce launch).  Off by default: every tile of a
-  // weight-gradient GEMM finishes in the last wave, so the fused reductions run on one CU per tile
-  // at the end of the launch — TN b3 512x512x19200 58 -> 93 us, the step 4.65 -> 5.43 ms
-  // (profiles/r04/splitk_fused_ab.txt) — where the separate launch spreads them over every CU.
-  static int fused_env = -1;
-  if (fused_env < 0) {
-    const char* e = getenv("JMT_SPLITK_FUSED");
-    fused_env = (e && e[0] == '1') ? 1 : 0;
-  }
-  p.counters = nullptr;
-  if (splits > 1 && fused_env) {
-    p.counters = (int*)((char*)d->workspace + splitk_slab_bytes(d->M, d->N, batch0 * batch1,
-                                                                splits));
-    const size_t cb = (size_t)p.tiles_m * p.tiles_n * batch0 * batch1 * sizeof(int);
-    if (hipMemsetAsync(p.counters, 0, cb, st) != hipSuccess)
-      return set_error(JMT_ERR_HIP, "jmt_gemm: counter memset failed");
-  }
   dim3 grid(p.tiles_m * p.tiles_n, batch0 * batch1, splits);
   if (dt == JMT_F32) launch_t<float>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
   else if (dt == JMT_BF16) launch_t<__bf16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
   else launch_t<_Float16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
   JMT_LAUNCH_CHECK("jmt_gemm");
-  if (splits > 1 && !p.counters) {
+  if (splits > 1) {
     const bool v4 = d->N % 4 == 0 && p.c_vec4;
     const int64_t total = (int64_t)d->M * d->N * batch0 * batch1 / (v4 ? 4 : 1);
     int blocks = (int)((total + 255) / 256);

@@ -1,4 +1,4 @@
-// Persistent form of the GEMM (jmt_gemm cfg 40 / 41): one block per CU walks whole output
+// Persistent form of the GEMM (jmt_gemm cfg 40): one block per CU walks whole output
 // tiles with one continuous LDS-DMA pipeline (details at gemm_persist_kernel).
 #include "gemm_tile.h"
 
@@ -20,8 +20,8 @@ namespace jmt {
 // only takes full tiles (straight-line epilogue: TM * TN / 2 16-B stores per wave, no loads —
 // the bias comes from LDS, staged once per launch).
 // Preconditions (jmt_gemm, persist_ok): 16-bit A, B and C, M % BM == N % BN == 0, K % BKE == 0,
-// C rows 16-B aligned, no split-K, beta = 0, no ReLU mask operand, no row sums, bias per column
-// (tables of at most kPersistBias floats in all).
+// C rows 16-B aligned, no split-K, no row sums, bias per column (tables of at most kPersistBias
+// floats in all); beta * C and the ReLU mask are compile-time epilogue forms (EPI).
 
 // s_waitcnt vmcnt(VMT * k + (st ? NST : 0)) for wave-uniform 0 <= k <= K
 template <int VMT, int NST, int K>
@@ -308,130 +308,11 @@ void gemm_persist_kernel(GemmParams p) {
   }
 }
 
-// cfg 42: the 128-B-K-tile pipeline with the A operand three-deep.  The A panel streams from
-// HBM (each 256-row panel is read by only N / 256 blocks), the B panel (weights) from L2, and
-// with one K-tile in flight the skip-MFMA ablation of cfg 40 ran 32.5 of its 51 us (NT
-// 19200x512x512 b3, profiles/r04/gemm_persist_ablate.jsonl): the pipeline waited on HBM latency.
-// LDS = 3 A images + 2 B images of 32 KiB = the whole 160 KiB, so the bias comes from scalar
-// loads.  Per iteration s: DMA A(s + 2), B(s + 1) -> wait for B(s) (issued after A(s + 1), so
-// A(s) is older and landed with it) -> barrier -> MFMAs -> barrier -> epilogue at a tile's end.
-template <typename T, bool AK, bool BK, class C, int EPI>
-__global__ __launch_bounds__(C::NT, C::OCC)
-void gemm_persist3_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  static_assert(C::BM == 256 && C::BN == 256 && C::S == 2 && !C::IL, "cfg 40 geometry");
-  constexpr int BKE = C::KB / (int)sizeof(T);
-  constexpr int IA = C::BM * C::KB;
-  constexpr int IB = C::BN * C::KB;
-  constexpr int NWV = C::NT / 64;
-  constexpr int NIA = C::BM * C::KB / 1024 / NWV;
-  constexpr int NIB = C::BN * C::KB / 1024 / NWV;
-  constexpr int NST = C::TM * (C::TN / 2);
-  static_assert(NIA + NIB + NST < 64, "vmcnt range");
-  static_assert(3 * IA + 2 * IB <= 160 * 1024, "LDS");
-  char* const imgA0 = smem;
-  char* const imgB0 = smem + 3 * IA;
-
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int wm = wid / C::WN, wn = wid % C::WN;
-  const int W = p.tiles_m * p.tiles_n * p.batch0 * p.batch1;
-  const int G = gridDim.x;
-  const int nm = (W - (int)blockIdx.x + G - 1) / G;
-  const int nkt = p.K / BKE;
-  const int total = nm * nkt;
-
-  uint32_t offa[NIA], offb[NIB];
-  glds_offsets<T, AK, C::KB, C::BM, C::NT>(offa, p.lda, 1 << 30, 0);
-  glds_offsets<T, BK, C::KB, C::BN, C::NT>(offb, p.ldb, 1 << 30, 0);
-  // issue cursors: A runs two K-tiles ahead, B one
-  struct Cursor {
-    int k, kt;
-    PItem it;
-  };
-  Cursor ca{0, 0, pitem(p, blockIdx.x, W)}, cb{0, 0, pitem(p, blockIdx.x, W)};
-  auto advance = [&](Cursor& c) {
-    if (++c.kt == nkt) {
-      c.kt = 0;
-      if (++c.k < nm) c.it = pitem(p, blockIdx.x + c.k * G, W);
-    }
-  };
-  auto issue_a = [&](int t) {
-    int ka;
-    const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, ca.it.b0, ca.it.b1, p.a_kseg,
-                                 ca.kt * BKE, ka);
-    const char* sa = (const char*)(AK ? A + (int64_t)ca.it.m0 * p.lda + ka
-                                      : A + (int64_t)ka * p.lda + ca.it.m0);
-    char* img = imgA0 + (t % 3) * IA;
-#pragma unroll
-    for (int i = 0; i < NIA; ++i) glds_slot<NIA>(img, sa, offa, i);
-    advance(ca);
-  };
-  auto issue_b = [&](int t) {
-    int kb;
-    const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, cb.it.b0, cb.it.b1, p.b_kseg,
-                                 cb.kt * BKE, kb);
-    const char* sb = (const char*)(BK ? B + (int64_t)cb.it.n0 * p.ldb + kb
-                                      : B + (int64_t)kb * p.ldb + cb.it.n0);
-    char* img = imgB0 + (t & 1) * IB;
-#pragma unroll
-    for (int i = 0; i < NIB; ++i) glds_slot<NIB>(img, sb, offb, i);
-    advance(cb);
-  };
-  // prologue: A(0), A(1), B(0) — so that B(s) is always issued after A(s + 1)
-  issue_a(0);
-  if (total > 1) issue_a(1);
-  issue_b(0);
-
-  f32x4 acc[C::TM][C::TN];
-#pragma unroll
-  for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  PItem cur = pitem(p, blockIdx.x, W);
-  int cur_k = 0, cur_kt = 0;
-  int last_ep = -(1 << 20);
-  const bool count_stores = !(p.dbg & (32 | 2));
-
-  for (int s = 0; s < total; ++s) {
-    // A(s + 2)'s buffer (s - 1) % 3 and B(s + 1)'s buffer (s - 1) & 1 were freed by the second
-    // barrier of iteration s - 1
-    const bool ga = s + 2 < total, gb = s + 1 < total;
-    if (ga) issue_a(s + 2);
-    if (gb) issue_b(s + 1);
-    // younger than B(s): this iteration's DMA and the stores of an epilogue at the end of s - 1
-    const bool st = count_stores && s <= last_ep + 1;
-    if (ga) {
-      if (st) wait_vmcnt<NIA + NIB + NST>();
-      else wait_vmcnt<NIA + NIB>();
-    } else if (gb) {
-      if (st) wait_vmcnt<NIB + NST>();
-      else wait_vmcnt<NIB>();
-    } else {
-      if (st) wait_vmcnt<NST>();
-      else wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    if (!(p.dbg & 1))
-      compute_tile<T, AK, BK, C>(imgA0 + (s % 3) * IA, imgB0 + (s & 1) * IB, wm, wn, acc);
-    __builtin_amdgcn_s_barrier();
-    if (++cur_kt == nkt) {
-      if (!(p.dbg & 2)) persist_epilogue<T, C, EPI>(p, cur, acc, nullptr, lane, wm, wn);
-#pragma unroll
-      for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-        for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      last_ep = s;
-      cur_kt = 0;
-      if (++cur_k < nm) cur = pitem(p, blockIdx.x + cur_k * G, W);
-    }
-  }
-}
-
-// persistent configurations (gemm_persist_kernel): cfg 40 = Cfg5's tile (128-B K-tiles, 2
-// stages), cfg 41 = Cfg20's (64-B K-tiles, 4 stages, DMA issue interleaved with the MFMAs)
+// the persistent configuration (gemm_persist_kernel): cfg 40 = Cfg5's tile (128-B K-tiles, 2
+// stages).  (Cfg20's 64-B K-tiles in 4 stages with interleaved DMA issue — "cfg 41" — and a
+// three-deep A ring with the bias from scalar loads — "cfg 42" — measured slower on every step
+// shape: profiles/r04/gemm_persist_vs_vendor_a.jsonl, gemm_persist_forced_ab.txt.)
 using Cfg40 = Cfg5;
-using Cfg41 = Cfg20;
 
 static int num_cus() {
   static int cache[64] = {0};
@@ -446,11 +327,9 @@ static int num_cus() {
   return cache[dev];
 }
 
-template <typename T, bool AK, bool BK, class C, bool A3, int EPI>
+template <typename T, bool AK, bool BK, class C, int EPI>
 static void launch_persist_epi(const GemmParams& p, int blocks, hipStream_t st) {
-  void (*fn)(GemmParams);
-  if constexpr (A3) fn = gemm_persist3_kernel<T, AK, BK, C, EPI>;
-  else fn = gemm_persist_kernel<T, AK, BK, C, EPI>;
+  void (*fn)(GemmParams) = gemm_persist_kernel<T, AK, BK, C, EPI>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -459,42 +338,34 @@ static void launch_persist_epi(const GemmParams& p, int blocks, hipStream_t st) 
   }
   int nb = 0;
   if (p.bias_mode == 1) nb = (p.n_bias > 0 ? p.batch0 : 1) * p.N;
-  const size_t lds = A3 ? (size_t)3 * C::BM * C::KB + (size_t)2 * C::BN * C::KB
-                       : (size_t)C::S * C::STAGE + (size_t)nb * sizeof(float);
+  const size_t lds = (size_t)C::S * C::STAGE + (size_t)nb * sizeof(float);
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(C::NT), lds, st, p);
 }
 
-template <typename T, bool AK, bool BK, class C, bool A3>
+template <typename T, bool AK, bool BK, class C>
 static void launch_persist_cfg(const GemmParams& p, int blocks, hipStream_t st) {
   const int epi = (p.beta != 0.f ? 1 : 0) | (p.aux != nullptr ? 2 : 0);
   switch (epi) {
-    case 0: launch_persist_epi<T, AK, BK, C, A3, 0>(p, blocks, st); break;
-    case 1: launch_persist_epi<T, AK, BK, C, A3, 1>(p, blocks, st); break;
-    case 2: launch_persist_epi<T, AK, BK, C, A3, 2>(p, blocks, st); break;
-    default: launch_persist_epi<T, AK, BK, C, A3, 3>(p, blocks, st); break;
+    case 0: launch_persist_epi<T, AK, BK, C, 0>(p, blocks, st); break;
+    case 1: launch_persist_epi<T, AK, BK, C, 1>(p, blocks, st); break;
+    case 2: launch_persist_epi<T, AK, BK, C, 2>(p, blocks, st); break;
+    default: launch_persist_epi<T, AK, BK, C, 3>(p, blocks, st); break;
   }
 }
 
-template <typename T, class C, bool A3 = false>
+template <typename T, class C>
 static void launch_persist_t(const GemmParams& p, int ak, int bk, int blocks, hipStream_t st) {
-  if (ak && bk) launch_persist_cfg<T, true, true, C, A3>(p, blocks, st);
-  else if (ak) launch_persist_cfg<T, true, false, C, A3>(p, blocks, st);
-  else if (bk) launch_persist_cfg<T, false, true, C, A3>(p, blocks, st);
-  else launch_persist_cfg<T, false, false, C, A3>(p, blocks, st);
+  if (ak && bk) launch_persist_cfg<T, true, true, C>(p, blocks, st);
+  else if (ak) launch_persist_cfg<T, true, false, C>(p, blocks, st);
+  else if (bk) launch_persist_cfg<T, false, true, C>(p, blocks, st);
+  else launch_persist_cfg<T, false, false, C>(p, blocks, st);
 }
 
 int launch_gemm_persist(const GemmParams& p, int dt, int ak, int bk, int cfg, int blocks,
                         hipStream_t st) {
-  if (cfg == 40) {
-    if (dt == JMT_BF16) launch_persist_t<__bf16, Cfg40>(p, ak, bk, blocks, st);
-    else launch_persist_t<_Float16, Cfg40>(p, ak, bk, blocks, st);
-  } else if (cfg == 42) {
-    if (dt == JMT_BF16) launch_persist_t<__bf16, Cfg40, true>(p, ak, bk, blocks, st);
-    else launch_persist_t<_Float16, Cfg40, true>(p, ak, bk, blocks, st);
-  } else {
-    if (dt == JMT_BF16) launch_persist_t<__bf16, Cfg41>(p, ak, bk, blocks, st);
-    else launch_persist_t<_Float16, Cfg41>(p, ak, bk, blocks, st);
-  }
+  (void)cfg;   // 40
+  if (dt == JMT_BF16) launch_persist_t<__bf16, Cfg40>(p, ak, bk, blocks, st);
+  else launch_persist_t<_Float16, Cfg40>(p, ak, bk, blocks, st);
   return 0;
 }
 
@@ -514,9 +385,9 @@ int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int 
                   d->M % 256 == 0 && d->N % 256 == 0 && d->K % 64 == 0 && d->K >= 128 &&
                   p.c_vec8 && p.c_vec4 && p.bias_mode != 2 && nbias <= kPersistBias;
   if (!ok) return 0;
-  if (forced >= 40 && forced <= 42) return forced;
+  if (forced == 40) return forced;
   if (forced != 0 || env == 0) return 0;
-  if (env >= 40 && env <= 42) return env;
+  if (env == 40) return env;
   // default: the 128-B-K-tile form wherever the launch has at least 1.5 tiles per CU (below
   // that the 160x256 / split tiles of the one-block-per-tile kernel quantise better: NT
   // 19200x512x2048 53 vs 68 us); it beat the one-block-per-tile kernel on every batched step

@@ -40,9 +40,6 @@ struct GemmParams {
   float* dbias_tab[MAXP];
   float* dbias_ws;
   int n_dbias, dbias_acc;
-  // split-K reduced inside the launch (splitk_fixup): per (batch, tile) arrival counters, zeroed
-  // before the launch; nullptr = the separate splitk_reduce_kernel
-  int* counters;
 };
 
 // PF: A-fragment prefetch distance in MFMA rows; PRIO: s_setprio(1) around each MFMA row;
@@ -82,12 +79,10 @@ using Cfg21 = TileCfg<128, 128, 2, 2, 64, 4, 1, 1, 0, 2, 1>;
 // 512-wide output is 240 tiles — 0.94 of one wave on 256 CUs where the 256x256 tile leaves 150
 // (0.59 of a wave, 41 % of the CUs idle) and batched launches quantise to 94 % instead of 88 %.
 // K-major A only (the MN-major image swizzle needs a power-of-two row count); the 20 A
-// instructions of a K-tile are dealt round-robin over the 8 waves (glds_tile, dma_count).
-using Cfg30 = TileCfg<160, 256, 2, 4, 128, 2, 1, 1, 0>;
-// the same tile with more K-steps in flight for the long-K single B*T-row GEMMs (hipBLASLt fills
-// its LDS ~1.8x faster per CU there): 64-B K-tiles in 4 stages (3 in flight, 106 KiB)
-// or 128-B K-tiles in 3 stages (2 in flight, 156 KiB); uneven DMA dealing, per-wave waits
-using Cfg31 = TileCfg<160, 256, 2, 4, 64, 4, 1, 1, 0>;
+// instructions of a K-tile are dealt round-robin over the 8 waves (glds_tile, dma_count);
+// 128-B K-tiles in 3 stages (two K-steps in flight, 156 KiB; uneven DMA dealing, per-wave
+// waits).  (2 stages, round 3's form, and 64-B K-tiles in 4 stages measured 1 % / 12-17 % slower:
+// profiles/r04/gemm_tile160_stages.txt.)
 using Cfg32 = TileCfg<160, 256, 2, 4, 128, 3, 1, 1, 0>;
 // (256x256 over 4 waves — 2x2, 128x128 each, 256 accumulators per lane in AGPRs, 64-B K-tiles,
 // 4 stages, one block / CU: the macro tile hipBLASLt picks on these shapes, profiles/
@@ -564,14 +559,14 @@ __device__ __forceinline__ void load4_guard(const O* row, int n, int lim, bool v
   }
 }
 
-// gemm_persist.hip: launch the persistent kernel (cfg 40 / 41) on `blocks` blocks
+// gemm_persist.hip: launch the persistent kernel (cfg 40) on `blocks` blocks
 int launch_gemm_persist(const GemmParams& p, int dt, int ak, int bk, int cfg, int blocks,
                         hipStream_t st);
 int num_cus_persist();
-// the persistent configuration (40 / 41) jmt_gemm launches for this descriptor, 0 = none:
-// `forced` is jmt_gemm_set_debug's forced tile config (40 / 41 take the persistent kernel where
-// its preconditions hold); otherwise JMT_GEMM_PERSIST (0 off, 40 / 41 every eligible launch,
-// unset: the measured default by layout and shape)
+// the persistent configuration (40) jmt_gemm launches for this descriptor, 0 = none: `forced`
+// is jmt_gemm_set_debug's forced tile config (40 takes the persistent kernel where its
+// preconditions hold); otherwise JMT_GEMM_PERSIST (0 off, 40 every eligible launch, unset: the
+// measured default by layout and shape)
 int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int forced);
 // gemm_persist_kernel's limit on the per-column bias staged in LDS (floats, all tables)
 constexpr int kPersistBias = 8192;

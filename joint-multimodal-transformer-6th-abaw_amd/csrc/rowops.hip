@@ -1127,11 +1127,8 @@ extern "C" int jmt_layernorm_bwd_grouped(int dt_in, int dt_dy, int dt_dx, int G,
   hipStream_t st = as_stream(stream);
   const int nblk = jmt_layernorm_bwd_grouped_blocks(rows);
   const dim3 grid((unsigned)nblk, (unsigned)G);
-  // development A/B: rows in flight per wave (JMT_LN_BWD_U=4; D = 512, one dtype throughout)
-  static const int ln_u = [] {
-    const char* e = getenv("JMT_LN_BWD_U");
-    return (e && atoi(e) == 4) ? 4 : 2;
-  }();
+  // (4 rows in flight per wave measured slower in isolation and equal in the step:
+  // profiles/r03_ln_bwd_u_ab.jsonl; 2 is the only form compiled)
 #define JMT_LNBG_U(NV, DS, U)                                                                    \
   hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV, DS, LN_ROWS_PER_BLOCK_GROUPED, U>), grid, \
                      dim3(RB), 0, st, rows,                                                     \
@@ -1141,11 +1138,8 @@ extern "C" int jmt_layernorm_bwd_grouped(int dt_in, int dt_dy, int dt_dx, int G,
   JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_dy, TG, JMT_DISPATCH1(dt_dx, TD,
       constexpr bool same = sizeof(TI) == 2 && std::is_same<TI, TG>::value &&
                             std::is_same<TI, TD>::value;
-      if (same && ln_u == 4 && D == 512) {
-        if constexpr (same) {
-          if (dsum) { JMT_LNBG_U(2, true, 4); } else { JMT_LNBG_U(2, false, 4); }
-        }
-      } else if (dsum) {
+      (void)same;
+      if (dsum) {
         if (D == 512) { JMT_LNBG(2, true); }
         else if (D == 768) { JMT_LNBG(3, true); }
         else { JMT_LNBG(4, true); }

@@ -906,27 +906,6 @@ def attn_backward(saved, go, dq, dk, dv):
         for buf, tmp in tmps.values():
             buf.copy_(tmp)
         return
-    if fused and ops._attn_km["on"]:
-        # P and dS handed over key-major, so dK = dS^T Q and dV = P^T dO read a K-major A
-        # operand (jmt_gemm's 160 x 256 tile; profiles/r03_dkdv.jsonl)
-        ldq = _round_up(Lq, 8)
-        bT = (H * Lk * ldq, Lk * ldq)
-        P = torch.empty(N * H * Lk * ldq, dtype=cd, device=dev)
-        dS = torch.empty(N * H * Lk * ldq, dtype=cd, device=dev)
-        ops.attn_bwd_km(_dc(cd), N, H, Lq, Lk, dh, go.data_ptr(), (so_l, so_n),
-                        o.data_ptr(), (o.stride(0), o.stride(1)),
-                        _ptr(q_src, qcol), (sq_l, sq_n), _ptr(k_src, kcol), (sk_l, sk_n),
-                        _ptr(v_src, vcol), (sv_l, sv_n), lse, P, dS, ldq,
-                        _ptr(dq, qcol), (dq.stride(0), dq.stride(1)), scale)
-        for A, B, sb, C, c0 in ((dS, q_src, (sq_l, sq_n), dk, kcol),
-                                (P, go, (so_l, so_n), dv, vcol)):
-            ops.gemm(M=Lk, N=dh, K=Lq, ab_dtype=_dc(cd), c_dtype=_dc(cd),
-                     a=[A.data_ptr()], lda=ldq, a_kmajor=True, sA=bT,
-                     b=[_ptr(B, qcol) if B is q_src else B.data_ptr()], ldb=sb[0],
-                     b_kmajor=False, sB=(sb[1], dh),
-                     c=[_ptr(C, c0)], ldc=C.stride(0), sC=(C.stride(1), dh), batch0=N,
-                     batch1=H, device=dev)
-        return
     if (fused and ops._attn_dkdv["on"] and _small_aligned(dk, kcol, cd)
             and _small_aligned(dv, vcol, cd)):
         # P and dS (rows of 128-key tiles) -> dK = dS^T Q and dV = P^T dO in one persistent kernel

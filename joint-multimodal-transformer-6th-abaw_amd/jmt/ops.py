@@ -335,22 +335,6 @@ def attn_short_bwd(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k
              "bytes": float(N * H) * ((4 * Lq + 4 * Lk) * dh * es + 4 * Lq)}, launch)
 
 
-_attn_km = {"on": os.environ.get("JMT_ATTN_KM", "0") == "1"}
-
-
-def attn_bwd_km(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k_ptr, sk, v_ptr,
-                sv, lse, p, ds, ldt, dq_ptr, sdq, scale):
-    """attn_bwd with P and dS written key-major (rows (n H + h) Lk + k, ldt >= Lq columns)."""
-    launch = lambda: _lib.call("jmt_attn_bwd_km", dtype, N, H, Lq, Lk, dh, go_ptr, sgo[0],
-                               sgo[1], o_ptr, so[0], so[1], q_ptr, sq[0], sq[1], k_ptr, sk[0],
-                               sk[1], v_ptr, sv[0], sv[1], lse.data_ptr(), p.data_ptr(),
-                               ds.data_ptr(), ldt, dq_ptr, sdq[0], sdq[1], scale, stream())
-    es = 4 if dtype == F32 else 2
-    _hooked({"family": "attn_bwd", "flops": 4.0 * N * H * Lq * Lk * dh,
-             "bytes": float(N * H) * ((4 * Lq + 2 * Lk) * dh * es + 4 * Lq + 2 * Lk * ldt * es)},
-            launch)
-
-
 SMALL_ATTN_MAX_L = 8
 
 

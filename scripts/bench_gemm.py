@@ -23,6 +23,9 @@ SHAPES = [
     ("fwd 19200x1024x512 NT", 19200, 1024, 512, True, True, 1, BF16, 1),
     ("fwd out1 19200x1024x3072 NT", 19200, 1024, 3072, True, True, 1, BF16, 1),
     ("dgrad 19200x512x512 NN", 19200, 512, 512, True, False, 1, BF16, 1),
+    ("dgrad b3 19200x512x512 NN", 19200, 512, 512, True, False, 3, BF16, 1),
+    ("fwd b6 19200x1024x512 NT", 19200, 1024, 512, True, True, 6, BF16, 1),
+    ("dgrad b6 19200x512x1024 NN", 19200, 512, 1024, True, False, 6, BF16, 1),
     ("dgrad out1 19200x3072x1024 NN", 19200, 3072, 1024, True, False, 1, BF16, 1),
     ("wgrad out1 1024x3072x19200 TN", 1024, 3072, 19200, False, False, 1, F32, None),
     ("wgrad 512x512x19200 TN", 512, 512, 19200, False, False, 1, F32, None),
@@ -97,7 +100,8 @@ if __name__ == "__main__":
                 us = s.elapsed_time(e) / 50 * 1e3
                 print(json.dumps({"op": name, "MB": mb, "us": round(us, 2), "gbs": round(by / us / 1e3, 1)}))
     if args.only:
-        SHAPES[:] = [s for s in SHAPES if args.only in s[0]]
+        keys = args.only.split(",")
+        SHAPES[:] = [s for s in SHAPES if any(k in s[0] for k in keys)]
     for c in args.cfg:
         for d in args.dbg:
             run(args.reps, d, c)

@@ -21,7 +21,7 @@ def header_functions():
 
 def test_library_loads_and_version():
     lib = _lib.load()
-    assert lib.jmt_abi_version() == 5
+    assert lib.jmt_abi_version() == 6
     assert lib.jmt_kernel_count() > 0
 
 
@@ -86,8 +86,8 @@ def test_argument_validation_fails_loudly():
 def test_workspace_size():
     lib = _lib.load()
     assert lib.jmt_gemm_workspace_bytes(512, 512, 1, 1) == 0
-    # fp32 slabs + one arrival counter per (batch, 128 x 128 tile), rounded to 256 B
-    assert lib.jmt_gemm_workspace_bytes(512, 512, 6, 4) == 4 * 6 * 512 * 512 * 4 + 512
+    # the fp32 partial slabs (ABI 6: no arrival counters)
+    assert lib.jmt_gemm_workspace_bytes(512, 512, 6, 4) == 4 * 6 * 512 * 512 * 4
 
 
 def test_missing_library_raises(tmp_path, monkeypatch):

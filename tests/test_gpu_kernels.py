@@ -63,7 +63,7 @@ def test_gemm_layouts_dtypes(dt, ak, bk):
         assert torch.isnan(C[:, N:]).all(), "wrote outside N"
 
 
-@pytest.mark.parametrize("cfg", [1, 5, 10, 11, 20, 21, 30, 31, 32])
+@pytest.mark.parametrize("cfg", [1, 5, 10, 11, 20, 21, 32])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 def test_gemm_forced_configs(cfg, ak, bk):
     """Every tile configuration of the planner forced on every operand layout (bf16), on ragged
@@ -195,7 +195,7 @@ def test_gemm_kconcat_and_pointer_tables(dt):
     assert (dW - ref).abs().max().item() <= _tol(dt, M) * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("cfg", [40, 41, 42])
+@pytest.mark.parametrize("cfg", [40])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 def test_gemm_persistent(cfg, ak, bk):
     """gemm_persist_kernel (csrc/gemm_persist.hip: one block per CU walks whole 256x256 tiles
@@ -542,42 +542,6 @@ def test_fused_attention_bwd_vs_fp32(cd, Lq, Lk, N):
     e_dq = (dq[..., E:2 * E].float() - dqr).abs().max().item()
     assert e_dq <= 16 * u * dqr.abs().max().item() + floor * kp.float().abs().max().item(), e_dq
     assert torch.isnan(dq[..., :E].float()).all() and torch.isnan(dq[..., 2 * E:].float()).all()
-
-
-def test_attn_bwd_rg2_bit_identical(tmp_path):
-    """JMT_ATTN_BWD_RG2=1 (csrc/attn_bwd2.hip: 4 waves, 32 query rows per wave) writes the same
-    P, dS and dQ bit for bit as the default 8-wave kernel (same per-row product order, same
-    canonical half-sum), at T = 300 / 1024, ragged 70 x 129 and Lk = 1 with more items than CUs."""
-    import subprocess
-    import sys
-    script = os.path.join(os.path.dirname(__file__), "_attn_rg2_eq.py")
-    f = str(tmp_path / "rg2.pt")
-    env = dict(os.environ, JMT_ATTN_BWD_RG2="0")
-    r = subprocess.run([sys.executable, script, "save", f], env=env, capture_output=True,
-                       text=True, timeout=180)
-    assert r.returncode == 0, r.stdout + r.stderr
-    env["JMT_ATTN_BWD_RG2"] = "1"
-    r = subprocess.run([sys.executable, script, "cmp", f], env=env, capture_output=True,
-                       text=True, timeout=180)
-    assert r.returncode == 0, r.stdout + r.stderr
-
-
-def test_gemm_splitk_fused_reduce_bit_identical(tmp_path):
-    """JMT_SPLITK_FUSED=1 (the last split block of each tile reduces it, gemm.hip splitk_fixup)
-    writes bit-identical outputs to the separate reduce launch; both run as child processes
-    (the switch is read once per process)."""
-    import subprocess
-    import sys
-    script = os.path.join(os.path.dirname(__file__), "_splitk_eq.py")
-    f = str(tmp_path / "sk.pt")
-    env = dict(os.environ, JMT_SPLITK_FUSED="1")
-    r = subprocess.run([sys.executable, script, "save", f], env=env, capture_output=True,
-                       text=True, timeout=180)
-    assert r.returncode == 0, r.stdout + r.stderr
-    env["JMT_SPLITK_FUSED"] = "0"
-    r = subprocess.run([sys.executable, script, "cmp", f], env=env, capture_output=True,
-                       text=True, timeout=180)
-    assert r.returncode == 0, r.stdout + r.stderr
 
 
 @pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
@@ -978,44 +942,6 @@ def test_head_kernels_vs_torch(k, dt):
         rb = 1.0 + G.sum(0)
         assert (db[i] - rb).abs().max().item() <= 1e-4 * max(1.0, rb.abs().max().item())
     assert torch.isnan(dh[:, 256:].float()).all(), "wrote past the two heads"
-
-
-@pytest.mark.parametrize("Lq,Lk,N", [(300, 300, 5), (70, 129, 3), (129, 1, 2), (33, 300, 4)])
-def test_fused_attention_bwd_keymajor_handoff(Lq, Lk, N):
-    """jmt_attn_bwd_km writes the same P and dS as jmt_attn_bwd, key-major (rows = keys, columns
-    = queries, stride ldt), and the same dq bit for bit; padding columns are never written."""
-    cd = torch.bfloat16
-    E = 512
-    g = torch.Generator(device=DEV).manual_seed(29)
-    qkv = torch.randn(N, Lq, 3 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
-    kv = torch.randn(N, Lk, 2 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
-    qp, kp, vp = qkv[..., :E], kv[..., :E], kv[..., E:]
-    scale = 1.0 / math.sqrt(E)
-    dt = ops.dt(qkv)
-    st = lambda t: (t.stride(0), t.stride(1))
-    o = torch.empty(Lq, N, E, device=DEV, dtype=cd)
-    lse = torch.empty(N * Lq, device=DEV, dtype=torch.float32)
-    ops.attn_fwd(dt, N, 1, Lq, Lk, E, qp.data_ptr(), st(qkv), kp.data_ptr(), st(kv),
-                 vp.data_ptr(), st(kv), o.data_ptr(), st(o), scale, lse)
-    go = torch.randn(Lq, N, E, device=DEV, generator=g).to(cd)
-    ldp, ldt = _rup(Lk, 8), _rup(Lq, 8) + 8
-    P = torch.empty(N * Lq * ldp, device=DEV, dtype=cd)
-    dS = torch.empty_like(P)
-    dq = torch.empty(Lq, N, E, device=DEV, dtype=cd)
-    args = (go.data_ptr(), st(go), o.data_ptr(), st(o), qp.data_ptr(), st(qkv), kp.data_ptr(),
-            st(kv), vp.data_ptr(), st(kv), lse)
-    ops.attn_bwd(dt, N, 1, Lq, Lk, E, *args, P, dS, ldp, dq.data_ptr(), st(dq), scale)
-    Pt = torch.full((N * Lk * ldt,), float("nan"), device=DEV, dtype=cd)
-    dSt = torch.full_like(Pt, float("nan"))
-    dq2 = torch.empty_like(dq)
-    ops.attn_bwd_km(dt, N, 1, Lq, Lk, E, *args, Pt, dSt, ldt, dq2.data_ptr(), st(dq2), scale)
-    torch.cuda.synchronize()
-    assert torch.equal(dq, dq2)
-    Pk = Pt.view(N, Lk, ldt)
-    dSk = dSt.view(N, Lk, ldt)
-    assert torch.equal(Pk[..., :Lq], P.view(N, Lq, ldp)[..., :Lk].transpose(1, 2))
-    assert torch.equal(dSk[..., :Lq], dS.view(N, Lq, ldp)[..., :Lk].transpose(1, 2))
-    assert torch.isnan(Pk[..., Lq:].float()).all() and torch.isnan(dSk[..., Lq:].float()).all()
 
 
 @pytest.mark.parametrize("dsum", [False, True])
