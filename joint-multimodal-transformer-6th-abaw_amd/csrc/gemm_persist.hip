@@ -59,7 +59,9 @@ __device__ __forceinline__ PItem pitem(const GemmParams& p, int w, int W) {
 // EPI: 0 plain, 1 beta * C, 2 ReLU mask (aux), 3 both — compile-time, so that every load the
 // epilogue issues is consumed on every path (a conditional load left hipcc unsure at the loop
 // head and it waited vmcnt(4) there, draining the next K-tile's DMA every iteration)
-template <typename T, class C, int EPI>
+// rows I0 .. I0 + NI - 1 of the wave's sub-tiles (the ping-pong kernel stores its two 64-row
+// halves in two segments)
+template <typename T, class C, int EPI, int I0 = 0, int NI = C::TM>
 __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PItem& it,
                                                  f32x4 (&acc)[C::TM][C::TN],
                                                  const float* bias_lds, int lane, int wm, int wn) {
@@ -123,13 +125,13 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
       if constexpr (lda_) a[j] = *(const u32x2*)(auxp + cbase + (int64_t)m * p.ldaux + n);
     }
   };
-  if constexpr (ldc_ || lda_) load_row(0, cr[0], ar[0]);
+  if constexpr (ldc_ || lda_) load_row(I0, cr[I0 & 1], ar[I0 & 1]);
 #pragma unroll
-  for (int i = 0; i < C::TM; ++i) {
+  for (int i = I0; i < I0 + NI; ++i) {
     const int m = it.m0 + wm * C::WTM + 16 * i + rl;
     const int64_t rowo = cbase + (int64_t)m * p.ldc;
     if constexpr (ldc_ || lda_)
-      if (i + 1 < C::TM) load_row(i + 1, cr[(i + 1) & 1], ar[(i + 1) & 1]);
+      if (i + 1 < I0 + NI) load_row(i + 1, cr[(i + 1) & 1], ar[(i + 1) & 1]);
 #pragma unroll
     for (int jp = 0; jp < C::TN / 2; ++jp) {
       uint32_t pk[2][2];
@@ -170,7 +172,8 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
   }
 }
 
-template <typename T, bool AK, bool BK, class C, int EPI>
+// ABL: development ablation (compute_tile MODE; dbg 64 -> 1, 128 -> 2), bf16 plain epilogue only
+template <typename T, bool AK, bool BK, class C, int EPI, int ABL = 0>
 __global__ __launch_bounds__(C::NT, C::OCC)
 void gemm_persist_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -276,7 +279,7 @@ void gemm_persist_kernel(GemmParams p) {
     __builtin_amdgcn_s_barrier();
     const char* img = smem + (s % C::S) * C::STAGE;
     if constexpr (C::S == 2) {
-      if (!(p.dbg & 1)) compute_tile<T, AK, BK, C>(img, img + IA, wm, wn, acc);
+      if (!(p.dbg & 1)) compute_tile<T, AK, BK, C, NoIssue, ABL>(img, img + IA, wm, wn, acc);
       __builtin_amdgcn_s_barrier();                    // buffer s & 1 free for K-tile s + 2
     } else {
       // piece q of the next K-tile's NIA + NIB DMA instructions goes before MFMA row
@@ -308,6 +311,326 @@ void gemm_persist_kernel(GemmParams p) {
   }
 }
 
+// ------------------------------------------------------------------ ping-pong kernel (cfg 43)
+// The persistent 256x256 tile with the DMA issue taken off the MFMA-issuing wave's critical
+// path.  Measured on cfg 40 (profiles/r05/gemm_ablate_*.jsonl): its time is the sum of a
+// DMA-only run and an MFMA-only run (NT b6 19200x1024x512: 64 + 70 -> 135 us without the
+// epilogue) at every pipeline depth (2 or 4 stages): the waves that issue the next K-tile's
+// LDS-DMA are the waves whose MFMAs then wait behind that issue, so no depth hides it.
+// Here (cdna_hip_programming.md §5 "The 256² 8-phase template"): the two waves of each SIMD
+// — group 0 = waves 0-3 (M rows 0-127 of the tile), group 1 = waves 4-7 (rows 128-255) — run
+// the same phase sequence one barrier apart (group 1 starts with one extra s_barrier), so
+// between any two barriers one group issues the next phase's LDS reads and its share of the
+// LDS-DMA stream while the other group's 16 MFMAs run on the same SIMD.
+//  * K-tile = 64 deep, staged as two k-halves (32 deep); a k-half slot holds A (256 x 64 B) and
+//    B (256 x 64 B) images = 32 KiB; PP_NSLOT slots in a ring (k-half g in slot g % PP_NSLOT).
+//  * Phases per K-tile (per wave): (ks, qm) = (0,0) (0,1) (1,0) (1,1): 4 row sub-tiles
+//    (qm half of the wave's 128 rows) x 4 column sub-tiles x one 32-deep k-step = 16 MFMAs;
+//    reads: 4 A fragments, + 4 B fragments when qm = 0 (B reused by qm = 1).
+//  * DMA stream: piece P = 8 KiB (8 wave-instructions) = one half of one operand's k-half
+//    image; interval I (between barriers I-1 and I; group I & 1 loads) issues piece I + PP_D,
+//    2 instructions per wave of the loading group.  k-half g must be retired (counted vmcnt by
+//    every issuing wave) before barrier 4g - 1 (group 0 reads it in interval 4g); its slot is
+//    free after barrier 4g + 4 - 4 * PP_NSLOT: PP_D = 4 PP_NSLOT - 5 keeps both.
+//  * Waits: the compiler never sees the DMA (inline asm); each wave counts its own VMEM issue
+//    (DMA pairs, epilogue stores / loads) and waits vmcnt(issued since its last piece of g) at
+//    the deadline; vmcnt counts in issue order, so rounding that count down (wait_vm_le) only
+//    over-waits.
+constexpr int PP_NSLOT = 4;
+constexpr int PP_D = 4 * PP_NSLOT - 5;
+static_assert(PP_D == 11, "pp_run's deadline counts (epilogue halves vs pieces per segment) are derived for PP_D = 11");
+constexpr int PP_SLOT = 32768;
+using CfgPP = TileCfg<256, 256, 2, 4, 64, 2, 1, 1, 0>;    // epilogue geometry (128 x 64 / wave)
+
+// s_waitcnt vmcnt(m) for the largest m <= n among 0..16, 20, 24, ..., 60 (wave-uniform n)
+__device__ __forceinline__ void wait_vm_le(int n) {
+  if (n <= 16) {
+    wait_vm(n);
+    return;
+  }
+  switch (n >= 60 ? 15 : n >> 2) {
+    case 4: wait_vmcnt<16>(); break;
+    case 5: wait_vmcnt<20>(); break;
+    case 6: wait_vmcnt<24>(); break;
+    case 7: wait_vmcnt<28>(); break;
+    case 8: wait_vmcnt<32>(); break;
+    case 9: wait_vmcnt<36>(); break;
+    case 10: wait_vmcnt<40>(); break;
+    case 11: wait_vmcnt<44>(); break;
+    case 12: wait_vmcnt<48>(); break;
+    case 13: wait_vmcnt<52>(); break;
+    case 14: wait_vmcnt<56>(); break;
+    default: wait_vmcnt<60>(); break;
+  }
+}
+
+// One group's whole schedule (GRP = 0: waves 0-3, 1: waves 4-7), everything that depends on
+// the group compile-time: which pieces it issues, where its stream moves to the next K-tile,
+// where its deadline waits go.  Per load segment the scalar work is a few adds: the wave's
+// four DMA sources are per-lane pointers (VGPRs) advanced by one VALU add per K-tile; the
+// item / K-concat bookkeeping runs once per K-tile of the stream.
+// development: s_memtime stamps of one block's segments (dbg 8, bf16 EPI 0 only; read with
+// jmt_gemm_pp_stamps_read): [wave][K-tile < PP_STK][phase][6]
+constexpr int PP_STK = 24;
+__device__ uint64_t g_pp_stamps[8 * PP_STK * 4 * 6];
+
+template <typename T, bool AK, bool BK, int EPI, int GRP, bool STAMP = false>
+__device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const float* bias_lds,
+                                       int nm, int W) {
+  using C = CfgPP;
+  typedef typename Frag16<T>::t F;
+  constexpr int HK = 32;                                   // k per k-half
+  constexpr int NST = C::TM * (C::TN / 2);                 // epilogue stores per wave
+  constexpr int NLD = ((EPI & 1) ? C::TM * C::TN : 0) + ((EPI & 2) ? C::TM * C::TN : 0);
+  constexpr int SUB = (GRP + PP_D) & 1;                    // parity of this group's pieces
+  // VMEM operations younger than the wave's last piece of k-half g at its deadline, away from
+  // the stream's end: its pieces of the load intervals (4g + 2 + SUB - PP_D, 4g - 2 + GRP]
+  constexpr int NSTEADY = 2 * ((PP_D - 4 + GRP - SUB) >> 1);
+  constexpr int EPH = (NST + NLD) / 2;                      // VMEM operations per epilogue half
+  constexpr int NSTEADY_EP1 = NSTEADY + EPH < 63 ? NSTEADY + EPH : 63;
+  constexpr int NSTEADY_EP2 = NSTEADY + 2 * EPH < 63 ? NSTEADY + 2 * EPH : 63;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wl = wid & 3;
+  constexpr int wm = GRP;
+  const int wn = wl;
+  const int G = gridDim.x;
+  const int nkt = p.K / 64;
+  const int nT = nm * nkt;
+  const int npieces = 8 * nT;
+  const int ins0 = SUB * 8 + 2 * wl;
+
+  // per-lane byte offsets of this wave's instructions ins0, ins0 + 1 of each operand's k-half
+  // image, relative to the operand's K-tile base
+  int64_t offa[2], offb[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    int row, kk;
+    chunk_src<T, AK, 64, 256>((ins0 + e) * 64 + lane, row, kk);
+    offa[e] = (AK ? (int64_t)row * p.lda + kk : (int64_t)kk * p.lda + row) * (int64_t)sizeof(T);
+    chunk_src<T, BK, 64, 256>((ins0 + e) * 64 + lane, row, kk);
+    offb[e] = (BK ? (int64_t)row * p.ldb + kk : (int64_t)kk * p.ldb + row) * (int64_t)sizeof(T);
+  }
+  const int64_t da = (AK ? (int64_t)64 : (int64_t)64 * p.lda) * (int64_t)sizeof(T);   // K-tile
+  const int64_t db = (BK ? (int64_t)64 : (int64_t)64 * p.ldb) * (int64_t)sizeof(T);
+  const int64_t ha = da / 2, hb = db / 2;                                             // k-half
+  const int sega = p.a_mode == 2 ? p.a_kseg / 64 : 1 << 30;   // K-tiles per K-concat segment
+  const int segb = p.b_mode == 2 ? p.b_kseg / 64 : 1 << 30;
+
+  // the issue stream: item iss_k, K-tile iss_kt of it, per-lane sources pa / pb of that K-tile
+  PItem iss_it = pitem(p, blockIdx.x, W);
+  int iss_k = 0, iss_kt = 0, lefta = 0, leftb = 0;
+  const char* pa[2];
+  const char* pb[2];
+  auto set_stream = [&]() {
+    const int k0 = iss_kt * 64;
+    int ka, kb;
+    const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, iss_it.b0, iss_it.b1,
+                                 p.a_kseg, k0, ka);
+    const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, iss_it.b0, iss_it.b1,
+                                 p.b_kseg, k0, kb);
+    const char* sa = (const char*)(AK ? A + (int64_t)iss_it.m0 * p.lda + ka
+                                      : A + (int64_t)ka * p.lda + iss_it.m0);
+    const char* sb = (const char*)(BK ? B + (int64_t)iss_it.n0 * p.ldb + kb
+                                      : B + (int64_t)kb * p.ldb + iss_it.n0);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      pa[e] = sa + offa[e];
+      pb[e] = sb + offb[e];
+    }
+    lefta = sega - (ka >> 6);                              // K-tiles left in A's segment
+    leftb = segb - (kb >> 6);
+  };
+  auto next_ktile = [&]() {
+    if (++iss_kt == nkt) {
+      iss_kt = 0;
+      if (++iss_k < nm) {
+        iss_it = pitem(p, blockIdx.x + iss_k * G, W);
+        set_stream();
+      }
+    } else if (--lefta == 0 || --leftb == 0) {
+      set_stream();
+    } else {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        pa[e] += da;
+        pb[e] += db;
+      }
+    }
+  };
+  // this wave's two instructions of piece Q = (operand, half) of k-half g
+  auto issue = [&](int g, int q) {
+    char* dst = smem + (g & (PP_NSLOT - 1)) * PP_SLOT + (q >= 2 ? 16384 : 0) + ins0 * 1024;
+    const int h = g & 1;
+    if (q < 2) {
+      glds_asm(pa[0] + (h ? ha : 0), dst);
+      glds_asm(pa[1] + (h ? ha : 0), dst + 1024);
+    } else {
+      glds_asm(pb[0] + (h ? hb : 0), dst);
+      glds_asm(pb[1] + (h ? hb : 0), dst + 1024);
+    }
+  };
+  // k-half g retired by this wave, at the barrier 4g - 1; i_now = this wave's latest load
+  // interval (its piece issued).  Issued after its last piece of g: its pieces of the load
+  // intervals in (i_last, i_now] (2 each, while pieces exist) and an epilogue of this K-tile.
+  // neh: epilogue halves (EPH operations each) issued after the wave's last piece of g (the
+  // caller knows them from the schedule: 0, 1 or 2)
+  auto deadline = [&](int g, int i_now, int neh) {
+    if (g >= 2 * nT) return;
+    if (i_now <= npieces - 1 - PP_D) {                     // steady state: constant counts
+      if (neh == 0) wait_vmcnt<NSTEADY>();
+      else if (neh == 1) wait_vmcnt<NSTEADY_EP1>();
+      else wait_vmcnt<NSTEADY_EP2>();
+      return;
+    }
+    const int i_last = 4 * g + 2 + SUB - PP_D;
+    const int hi = min(i_now, npieces - 1 - PP_D);
+    const int n = (hi > i_last ? 2 * ((hi - i_last) >> 1) : 0) + neh * EPH;
+    wait_vm_le(n);
+  };
+
+  // prologue: this group's pieces among 0 .. PP_D-1, k-half 0 retired, one barrier for all
+  set_stream();
+#pragma unroll
+  for (int P = SUB; P < PP_D; P += 2) {
+    if (P >= 8 && P - 2 < 8) next_ktile();                 // (PP_D <= 16: K-tiles 0 and 1)
+    if (P < npieces) issue(P >> 2, P & 3);
+  }
+  deadline(0, -1, 0);
+  __builtin_amdgcn_s_barrier();
+  if constexpr (GRP == 1) __builtin_amdgcn_s_barrier();    // group 1 runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  f32x4 acc[C::TM][C::TN];
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  F fa[4], fb[4];
+  PItem cur = pitem(p, blockIdx.x, W);
+  int cur_k = 0, cur_left = nkt;
+  // epilogue of an item in two halves: rows 0-63 of the wave (quadrant qm = 0, final after
+  // phase 2 of the item's last K-tile) in that K-tile's phase-3 load segment, rows 64-127 in the
+  // next K-tile's phase-0 load segment — half the store burst per segment
+  bool epA = false, epB = false;
+
+  const bool stamping = STAMP && blockIdx.x == 0 && lane == 0;
+  for (int t = 0; t < nT; ++t) {
+#pragma unroll
+    for (int pp = 0; pp < 4; ++pp) {
+      const int ks = pp >> 1, qm = pp & 1;
+      const int I = 8 * t + 2 * pp + GRP;                  // this wave's load interval
+      auto stamp = [&](int e) {
+        if constexpr (STAMP) {
+          if (stamping && t < PP_STK)
+            g_pp_stamps[((wid * PP_STK + t) * 4 + pp) * 6 + e] = __builtin_amdgcn_s_memtime();
+        }
+      };
+      stamp(0);
+      // ---- load segment
+      if (pp == 0) {
+        epB = false;
+        if (cur_left == 0) {                               // previous item done: rows 64-127
+          if (!(p.dbg & 2))
+            persist_epilogue<T, C, EPI, 4, 4>(p, cur, acc, bias_lds, lane, wm, wn);
+#pragma unroll
+          for (int i = 4; i < C::TM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          cur = pitem(p, blockIdx.x + (++cur_k) * G, W);
+          cur_left = nkt;
+          epB = true;
+        }
+        --cur_left;
+        epA = false;
+      }
+      if (pp == 3 && cur_left == 0 && t + 1 < nT) {        // the item's last K-tile: rows 0-63
+        if (!(p.dbg & 2)) persist_epilogue<T, C, EPI, 0, 4>(p, cur, acc, bias_lds, lane, wm, wn);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        epA = true;
+      }
+      const char* slot = smem + ((2 * t + ks) & (PP_NSLOT - 1)) * PP_SLOT;
+      if (qm == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          fb[j] = read_frag16<T, BK, 64, 256>(slot + 16384, wn * C::WTN + 16 * j, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[i] = read_frag16<T, AK, 64, 256>(slot, wm * C::WTM + 64 * qm + 16 * i, 0);
+      stamp(1);
+      {
+        // piece P = I + PP_D: K-tile t + (L >> 3), k-half 2 (t + (L >> 3)) + ((L >> 2) & 1),
+        // quarter L & 3, L = 2 pp + GRP + PP_D (compile-time)
+        const int L = 2 * pp + GRP + PP_D;
+        const int Lp = 2 * pp - 2 + GRP + PP_D;
+        if (pp > 0 ? ((L >> 3) != (Lp >> 3)) : ((L >> 3) != ((L + 6) >> 3) - 1))
+          next_ktile();
+        if (!(p.dbg & 4) && I + PP_D < npieces) issue(2 * (t + (L >> 3)) + ((L >> 2) & 1), L & 3);
+      }
+      stamp(2);
+      // epilogue halves younger than the wave's last piece of the k-half due (a segment issues
+      // its epilogue half BEFORE its piece; counting one too many would under-wait): at phase 1
+      // both halves of an epilogue that finished at this K-tile's start; at phase 3 this K-tile's
+      // own first half, and for group 1 the second half of this K-tile's start (group 0's last
+      // piece of k-half 2t + 2 went out after it, in the same phase-0 segment)
+      const int neh = pp == 1 ? (epB ? 2 : 0)
+                              : (GRP == 1 && epB ? 1 : 0) + (epA ? 1 : 0);
+      if (GRP == 1 && (pp & 1) && !(p.dbg & 16)) deadline((I + 1) >> 2, I, neh);
+      stamp(3);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      stamp(4);
+      // ---- MFMA segment
+      __builtin_amdgcn_s_setprio(1);
+      if (!(p.dbg & 1)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[4 * qm + i][j] = mfma16(fb[j], fa[i], acc[4 * qm + i][j]);   // C^T sub-tiles
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (GRP == 0 && (pp & 1) && !(p.dbg & 16)) deadline((I + 2) >> 2, I, neh);
+      stamp(5);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if constexpr (GRP == 0) __builtin_amdgcn_s_barrier();    // balance group 1's extra barrier
+  if (!(p.dbg & 2)) persist_epilogue<T, C, EPI>(p, cur, acc, bias_lds, lane, wm, wn);
+}
+
+template <typename T, bool AK, bool BK, int EPI, bool STAMP = false>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* bias_lds = (float*)(smem + PP_NSLOT * PP_SLOT);
+  const int W = p.tiles_m * p.tiles_n * p.batch0 * p.batch1;
+  const int G = gridDim.x;
+  const int nm = (W - (int)blockIdx.x + G - 1) / G;
+  if (p.bias_mode == 1) {
+    const int nb = (p.n_bias > 0 ? p.batch0 : 1) * p.N;
+    for (int i = threadIdx.x; i < nb; i += 512) {
+      const int b = i / p.N;
+      bias_lds[i] = (p.n_bias > 0 ? p.bias_tab[b] : p.bias)[i - b * p.N];
+    }
+  }
+  __syncthreads();
+  if (nm <= 0 || p.K < 64) return;
+  if constexpr (STAMP) {
+    if ((threadIdx.x >> 6) < 4) pp_run<T, AK, BK, EPI, 0, true>(p, smem, bias_lds, nm, W);
+    else pp_run<T, AK, BK, EPI, 1, true>(p, smem, bias_lds, nm, W);
+  } else {
+    if ((threadIdx.x >> 6) < 4) pp_run<T, AK, BK, EPI, 0>(p, smem, bias_lds, nm, W);
+    else pp_run<T, AK, BK, EPI, 1>(p, smem, bias_lds, nm, W);
+  }
+}
+
 // the persistent configuration (gemm_persist_kernel): cfg 40 = Cfg5's tile (128-B K-tiles, 2
 // stages).  (Cfg20's 64-B K-tiles in 4 stages with interleaved DMA issue — "cfg 41" — and a
 // three-deep A ring with the bias from scalar loads — "cfg 42" — measured slower on every step
@@ -330,21 +653,43 @@ static int num_cus() {
 template <typename T, bool AK, bool BK, class C, int EPI>
 static void launch_persist_epi(const GemmParams& p, int blocks, hipStream_t st) {
   void (*fn)(GemmParams) = gemm_persist_kernel<T, AK, BK, C, EPI>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
+  if constexpr (EPI == 0 && sizeof(T) == 2) {
+    if (p.dbg & 64) fn = gemm_persist_kernel<T, AK, BK, C, EPI, 1>;
+    if (p.dbg & 128) fn = gemm_persist_kernel<T, AK, BK, C, EPI, 2>;
   }
+  (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
   int nb = 0;
   if (p.bias_mode == 1) nb = (p.n_bias > 0 ? p.batch0 : 1) * p.N;
   const size_t lds = (size_t)C::S * C::STAGE + (size_t)nb * sizeof(float);
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(C::NT), lds, st, p);
 }
 
+template <typename T, bool AK, bool BK, int EPI>
+static void launch_pp_epi(const GemmParams& p, int blocks, hipStream_t st) {
+  void (*fn)(GemmParams) = gemm_pp_kernel<T, AK, BK, EPI>;
+  if constexpr (EPI == 0 && sizeof(T) == 2)
+    if (p.dbg & 8) fn = gemm_pp_kernel<T, AK, BK, EPI, true>;
+  (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  int nb = 0;
+  if (p.bias_mode == 1) nb = (p.n_bias > 0 ? p.batch0 : 1) * p.N;
+  const size_t lds = (size_t)PP_NSLOT * PP_SLOT + (size_t)nb * sizeof(float);
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(512), lds, st, p);
+}
+
 template <typename T, bool AK, bool BK, class C>
-static void launch_persist_cfg(const GemmParams& p, int blocks, hipStream_t st) {
+static void launch_persist_cfg(const GemmParams& p, int blocks, hipStream_t st, int cfg) {
   const int epi = (p.beta != 0.f ? 1 : 0) | (p.aux != nullptr ? 2 : 0);
+  if (cfg == 43) {
+    switch (epi) {
+      case 0: launch_pp_epi<T, AK, BK, 0>(p, blocks, st); break;
+      case 1: launch_pp_epi<T, AK, BK, 1>(p, blocks, st); break;
+      case 2: launch_pp_epi<T, AK, BK, 2>(p, blocks, st); break;
+      default: launch_pp_epi<T, AK, BK, 3>(p, blocks, st); break;
+    }
+    return;
+  }
   switch (epi) {
     case 0: launch_persist_epi<T, AK, BK, C, 0>(p, blocks, st); break;
     case 1: launch_persist_epi<T, AK, BK, C, 1>(p, blocks, st); break;
@@ -354,22 +699,36 @@ static void launch_persist_cfg(const GemmParams& p, int blocks, hipStream_t st) 
 }
 
 template <typename T, class C>
-static void launch_persist_t(const GemmParams& p, int ak, int bk, int blocks, hipStream_t st) {
-  if (ak && bk) launch_persist_cfg<T, true, true, C>(p, blocks, st);
-  else if (ak) launch_persist_cfg<T, true, false, C>(p, blocks, st);
-  else if (bk) launch_persist_cfg<T, false, true, C>(p, blocks, st);
-  else launch_persist_cfg<T, false, false, C>(p, blocks, st);
+static void launch_persist_t(const GemmParams& p, int ak, int bk, int blocks, hipStream_t st,
+                             int cfg) {
+  if (ak && bk) launch_persist_cfg<T, true, true, C>(p, blocks, st, cfg);
+  else if (ak) launch_persist_cfg<T, true, false, C>(p, blocks, st, cfg);
+  else if (bk) launch_persist_cfg<T, false, true, C>(p, blocks, st, cfg);
+  else launch_persist_cfg<T, false, false, C>(p, blocks, st, cfg);
 }
 
 int launch_gemm_persist(const GemmParams& p, int dt, int ak, int bk, int cfg, int blocks,
                         hipStream_t st) {
-  (void)cfg;   // 40
-  if (dt == JMT_BF16) launch_persist_t<__bf16, Cfg40>(p, ak, bk, blocks, st);
-  else launch_persist_t<_Float16, Cfg40>(p, ak, bk, blocks, st);
+  if (dt == JMT_BF16) launch_persist_t<__bf16, Cfg40>(p, ak, bk, blocks, st, cfg);
+  else launch_persist_t<_Float16, Cfg40>(p, ak, bk, blocks, st, cfg);
   return 0;
 }
 
 int num_cus_persist() { return num_cus(); }
+
+}  // namespace jmt
+
+// development: copy the ping-pong kernel's segment stamps (jmt::g_pp_stamps, dbg 8) to the host
+extern "C" int jmt_gemm_pp_stamps_read(uint64_t* host, int n) {
+  const int cap = (int)(sizeof(jmt::g_pp_stamps) / sizeof(uint64_t));
+  if (n > cap) n = cap;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(host, HIP_SYMBOL(jmt::g_pp_stamps), sizeof(uint64_t) * n) != hipSuccess)
+    return -1;
+  return n;
+}
+
+namespace jmt {
 
 int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int forced) {
   static int env = -1;
@@ -385,9 +744,9 @@ int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int 
                   d->M % 256 == 0 && d->N % 256 == 0 && d->K % 64 == 0 && d->K >= 128 &&
                   p.c_vec8 && p.c_vec4 && p.bias_mode != 2 && nbias <= kPersistBias;
   if (!ok) return 0;
-  if (forced == 40) return forced;
+  if (forced == 40 || forced == 43) return forced;
   if (forced != 0 || env == 0) return 0;
-  if (env == 40) return env;
+  if (env == 40 || env == 43) return env;
   // default: the 128-B-K-tile form wherever the launch has at least 1.5 tiles per CU (below
   // that the 160x256 / split tiles of the one-block-per-tile kernel quantise better: NT
   // 19200x512x2048 53 vs 68 us); it beat the one-block-per-tile kernel on every batched step

@@ -422,7 +422,10 @@ __device__ __forceinline__ void rowsum_tile(const char* imgA, int wm, int wn, Ro
   }
 }
 
-template <typename T, bool AK, bool BK, class C, class ISSUE = NoIssue>
+// MODE (development ablations of the persistent kernel, gemm_persist.hip dbg 64 / 128): 1 = the
+// fragments are read from LDS once per K-tile row 0 and reused (MFMAs without the LDS reads),
+// 2 = the LDS reads without the MFMAs (one v_add per MFMA keeps the reads live)
+template <typename T, bool AK, bool BK, class C, class ISSUE = NoIssue, int MODE = 0>
 __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB, int wm, int wn,
                                              f32x4 (&acc)[C::TM][C::TN],
                                              const ISSUE& issue = ISSUE()) {
@@ -448,14 +451,14 @@ __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB,
     for (int idx = 0; idx < NR; ++idx) {
       const int ks = idx / C::TM, i = idx % C::TM;
       int nreads = 0;
-      if (i == C::TM - BPF && ks + 1 < KS) {
+      if (MODE != 1 && i == C::TM - BPF && ks + 1 < KS) {
 #pragma unroll
         for (int j = 0; j < C::TN; ++j)
           fb[(ks + 1) & 1][j] = read_frag16<T, BK, C::KB, C::BN>(imgB, wn * C::WTN + j * 16,
                                                                  ks + 1);
         nreads += BK ? C::TN : 2 * C::TN;
       }
-      if (idx + PF < NR) {
+      if (MODE != 1 && idx + PF < NR) {
         const int r = idx + PF;
         fa[r % (PF + 1)] = read_frag16<T, AK, C::KB, C::BM>(imgA, wm * C::WTM + (r % C::TM) * 16,
                                                            r / C::TM);
@@ -463,9 +466,20 @@ __device__ __forceinline__ void compute_tile(const char* imgA, const char* imgB,
       }
       issue(idx);                                   // interleaved LDS-DMA pieces (Cfg IL)
       if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
+      if constexpr (MODE == 2) {
 #pragma unroll
-      for (int j = 0; j < C::TN; ++j)
-        acc[i][j] = mfma16(fb[ks & 1][j], fa[idx % (PF + 1)], acc[i][j]);   // C^T tile
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j][0] += __builtin_bit_cast(float, __builtin_shufflevector(
+                              fb[ks & 1][j], fa[idx % (PF + 1)], 0, 8)) ;
+      } else if constexpr (MODE == 1) {
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = mfma16(fb[0][j], fa[0], acc[i][j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = mfma16(fb[ks & 1][j], fa[idx % (PF + 1)], acc[i][j]);   // C^T tile
+      }
       if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
       if constexpr (C::SGB) {
         sgb_ds_reads(nreads);                                                 // DS reads first

@@ -195,7 +195,7 @@ def test_gemm_kconcat_and_pointer_tables(dt):
     assert (dW - ref).abs().max().item() <= _tol(dt, M) * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("cfg", [40])
+@pytest.mark.parametrize("cfg", [40, 43])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 def test_gemm_persistent(cfg, ak, bk):
     """gemm_persist_kernel (csrc/gemm_persist.hip: one block per CU walks whole 256x256 tiles
@@ -283,6 +283,49 @@ def test_gemm_persistent(cfg, ak, bk):
             ref = Acat @ Bl_t2.transpose(1, 2)[i] + bias
             err = (res[i].float() - ref).abs().max().item()
             assert err <= 1e-2 * ref.abs().max().item(), (cfg, "kcat", i, err)
+
+
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_pingpong_bit_identical_to_persistent(ak, bk):
+    """The ping-pong persistent kernel (cfg 43: two wave groups one barrier apart, LDS-DMA
+    pieces on a counted-vmcnt schedule, the epilogue in two halves) accumulates every output in
+    the same k order as cfg 40: bit-identical C on step shapes with several items per block
+    (item boundaries inside the DMA stream), beta * C, the ReLU mask, bias tables — repeated
+    launches (a missed wait shows as a difference that comes and goes)."""
+    from jmt import _lib
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(43)
+    bf = torch.bfloat16
+    for (M, N, K, nb, beta, use_aux) in [(19200, 1024, 512, 2, 0.0, False),
+                                         (19200, 512, 1024, 2, 1.0, False),
+                                         (7680, 768, 192, 3, 0.0, True),
+                                         (4096, 512, 128, 5, 0.5, True)]:
+        A, Al, lda, sa = _operand(M, K, ak, BF16, batch=nb, gen=g)
+        Bs, Bl_t, ldb, sb = _operand(N, K, bk, BF16, batch=nb, gen=g)
+        bias = [torch.randn(N, device=DEV, generator=g) for _ in range(nb)]
+        C0 = torch.randn(nb, M, N, device=DEV, generator=g).to(bf)
+        aux = torch.randn(nb, M, N, device=DEV, generator=g).to(bf) if use_aux else None
+        outs = {}
+        for cfg in (40, 43, 43, 43):
+            C = C0.clone()
+            lib.jmt_gemm_set_debug(cfg << 8)
+            try:
+                ops.gemm(M=M, N=N, K=K, ab_dtype=BF16, c_dtype=BF16, a=[A.data_ptr()], lda=lda,
+                         a_kmajor=ak, sA=(sa, 0), b=[Bs.data_ptr()], ldb=ldb, b_kmajor=bk,
+                         sB=(sb, 0), c=[C.data_ptr()], ldc=N, sC=(M * N, 0), batch0=nb,
+                         bias_tab=bias, bias_mode=1, beta=beta, aux=aux, ldaux=N, splits=1,
+                         device=DEV)
+            finally:
+                lib.jmt_gemm_set_debug(0)
+            outs.setdefault(cfg, []).append(C)
+        for C in outs[43]:
+            assert torch.equal(C, outs[40][0]), (M, N, K, nb, beta, use_aux,
+                                                 int((C != outs[40][0]).sum()))
+        ref = (Al[0] @ Bl_t.transpose(1, 2)[0]) + bias[0] + beta * C0[0].float()
+        if use_aux:
+            ref = torch.where(aux[0].float() > 0, ref, torch.zeros_like(ref))
+        err = (outs[43][0][0].float() - ref).abs().max().item()
+        assert err <= 1e-2 * ref.abs().max().item(), (M, N, K, err)
 
 
 def test_gemm_large_bf16_linear_shape():
