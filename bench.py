@@ -178,8 +178,13 @@ class FamilyProbe:
         fam = {}
         # every probe step launches the same sequence: each launch position is timed by the
         # median over the probe steps (one disturbed launch does not move its family), then
-        # summed per family as if each step had run at those medians
+        # summed per family as if each step had run at those medians.  Checked: the family and
+        # flop count of every position agree across the steps; otherwise the per-launch sum
         n = len(self.rec) // probe_steps if len(self.rec) % probe_steps == 0 else 0
+        if n and any(self.rec[k * n + i][:2] != self.rec[i][:2]
+                     for k in range(1, probe_steps) for i in range(n)):
+            n = 0
+        same_sequence = bool(n)
         med = [statistics.median(ms(self.rec[k * n + i][3]) for k in range(probe_steps))
                for i in range(n)] if n else [ms(r[3]) for r in self.rec]
         for i, (f, fl, by, ev) in enumerate(self.rec[:n] if n else self.rec):
@@ -206,7 +211,8 @@ class FamilyProbe:
                 out[-1].update({"bound": "hbm", "gbps": round(gbs, 1),
                                 "hbm_frac": round(gbs / PEAK_HBM_GBS, 4)})
         out.sort(key=lambda r: -r["ms_per_step"])
-        return {"families": out, "event_pair_overhead_us": round(over * 1e3, 2)}
+        return {"families": out, "event_pair_overhead_us": round(over * 1e3, 2),
+                "per_position_medians": same_sequence}
 
     def dump(self, path: str, probe_steps: int):
         """Per-launch records of the last probe step (shape, family, overhead-corrected us)."""

@@ -185,6 +185,24 @@ __device__ __forceinline__ void glds16_asm(const void* src, const void* lds_dst)
 #endif
 }
 
+// glds16_asm with the destination as a wave-uniform 32-bit LDS address (no generic->LDS cast:
+// that cast costs a null check and a readfirstlane per instruction when the pointer is computed)
+__device__ __forceinline__ void glds16_at(const void* src, uint32_t lds_addr) {
+#if !defined(__OPTIMIZE__)
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)(uintptr_t)lds_addr,
+                                   16, 0, 0);
+#else
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_addr)
+      : "memory");
+#endif
+}
+
 // The same instruction from the builtin: hipcc counts it in its own s_waitcnt bookkeeping (and
 // drains it before transposed LDS reads, above).  The attention kernels load their row operands
 // (Q, dO) into registers with plain loads that hipcc waits for by counting the VMEM operations

@@ -167,7 +167,11 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
       typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
       const u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
       JMT_DCHECK(m < p.M && n + 8 <= p.N);
+#ifdef JMT_EPI_PLAIN
+      *(u32x4*)(cp + rowo + n) = v;
+#else
       __builtin_nontemporal_store(v, (u32x4*)(cp + rowo + n));
+#endif
     }
   }
 }
@@ -374,12 +378,11 @@ __device__ __forceinline__ void wait_vm_le(int n) {
 constexpr int PP_STK = 24;
 __device__ uint64_t g_pp_stamps[8 * PP_STK * 4 * 6];
 
-template <typename T, bool AK, bool BK, int EPI, int GRP, bool STAMP = false>
-__device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const float* bias_lds,
-                                       int nm, int W) {
+template <typename T, bool AK, bool BK, int EPI, int GRP, int MODE = 0>
+__device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, const char* smem,
+                                       const float* bias_lds, int nm, int W) {
   using C = CfgPP;
   typedef typename Frag16<T>::t F;
-  constexpr int HK = 32;                                   // k per k-half
   constexpr int NST = C::TM * (C::TN / 2);                 // epilogue stores per wave
   constexpr int NLD = ((EPI & 1) ? C::TM * C::TN : 0) + ((EPI & 2) ? C::TM * C::TN : 0);
   constexpr int SUB = (GRP + PP_D) & 1;                    // parity of this group's pieces
@@ -390,9 +393,11 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const fl
   constexpr int NSTEADY_EP1 = NSTEADY + EPH < 63 ? NSTEADY + EPH : 63;
   constexpr int NSTEADY_EP2 = NSTEADY + 2 * EPH < 63 ? NSTEADY + 2 * EPH : 63;
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // SGPR: LDS addresses scalar
   const int wl = wid & 3;
   constexpr int wm = GRP;
+  constexpr bool STAMP = MODE == 2;                        // MODE 1: ablations, 2: + stamps
+  const int dbg = MODE ? p.dbg : 0;
   const int wn = wl;
   const int G = gridDim.x;
   const int nkt = p.K / 64;
@@ -460,14 +465,14 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const fl
   };
   // this wave's two instructions of piece Q = (operand, half) of k-half g
   auto issue = [&](int g, int q) {
-    char* dst = smem + (g & (PP_NSLOT - 1)) * PP_SLOT + (q >= 2 ? 16384 : 0) + ins0 * 1024;
+    const uint32_t dst = lbase + (g & (PP_NSLOT - 1)) * PP_SLOT + (q >= 2 ? 16384 : 0) + ins0 * 1024;
     const int h = g & 1;
     if (q < 2) {
-      glds_asm(pa[0] + (h ? ha : 0), dst);
-      glds_asm(pa[1] + (h ? ha : 0), dst + 1024);
+      glds16_at(pa[0] + (h ? ha : 0), dst);
+      glds16_at(pa[1] + (h ? ha : 0), dst + 1024);
     } else {
-      glds_asm(pb[0] + (h ? hb : 0), dst);
-      glds_asm(pb[1] + (h ? hb : 0), dst + 1024);
+      glds16_at(pb[0] + (h ? hb : 0), dst);
+      glds16_at(pb[1] + (h ? hb : 0), dst + 1024);
     }
   };
   // k-half g retired by this wave, at the barrier 4g - 1; i_now = this wave's latest load
@@ -515,6 +520,12 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const fl
   bool epA = false, epB = false;
 
   const bool stamping = STAMP && blockIdx.x == 0 && lane == 0;
+  // ablation dbg 32: every epilogue stores to tile (0, 0) of batch 0 (L2-resident C)
+  auto epi_item = [&](const PItem& it) {
+    PItem e = it;
+    if (dbg & 32) e.m0 = e.n0 = e.b0 = e.b1 = 0;
+    return e;
+  };
   for (int t = 0; t < nT; ++t) {
 #pragma unroll
     for (int pp = 0; pp < 4; ++pp) {
@@ -531,8 +542,8 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const fl
       if (pp == 0) {
         epB = false;
         if (cur_left == 0) {                               // previous item done: rows 64-127
-          if (!(p.dbg & 2))
-            persist_epilogue<T, C, EPI, 4, 4>(p, cur, acc, bias_lds, lane, wm, wn);
+          if (!(dbg & 2))
+            persist_epilogue<T, C, EPI, 4, 4>(p, epi_item(cur), acc, bias_lds, lane, wm, wn);
 #pragma unroll
           for (int i = 4; i < C::TM; ++i)
 #pragma unroll
@@ -545,7 +556,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const fl
         epA = false;
       }
       if (pp == 3 && cur_left == 0 && t + 1 < nT) {        // the item's last K-tile: rows 0-63
-        if (!(p.dbg & 2)) persist_epilogue<T, C, EPI, 0, 4>(p, cur, acc, bias_lds, lane, wm, wn);
+        if (!(dbg & 2)) persist_epilogue<T, C, EPI, 0, 4>(p, epi_item(cur), acc, bias_lds, lane, wm, wn);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -569,7 +580,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const fl
         const int Lp = 2 * pp - 2 + GRP + PP_D;
         if (pp > 0 ? ((L >> 3) != (Lp >> 3)) : ((L >> 3) != ((L + 6) >> 3) - 1))
           next_ktile();
-        if (!(p.dbg & 4) && I + PP_D < npieces) issue(2 * (t + (L >> 3)) + ((L >> 2) & 1), L & 3);
+        if (!(dbg & 4) && I + PP_D < npieces) issue(2 * (t + (L >> 3)) + ((L >> 2) & 1), L & 3);
       }
       stamp(2);
       // epilogue halves younger than the wave's last piece of the k-half due (a segment issues
@@ -579,7 +590,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const fl
       // piece of k-half 2t + 2 went out after it, in the same phase-0 segment)
       const int neh = pp == 1 ? (epB ? 2 : 0)
                               : (GRP == 1 && epB ? 1 : 0) + (epA ? 1 : 0);
-      if (GRP == 1 && (pp & 1) && !(p.dbg & 16)) deadline((I + 1) >> 2, I, neh);
+      if (GRP == 1 && (pp & 1) && !(dbg & 16)) deadline((I + 1) >> 2, I, neh);
       stamp(3);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -587,7 +598,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const fl
       stamp(4);
       // ---- MFMA segment
       __builtin_amdgcn_s_setprio(1);
-      if (!(p.dbg & 1)) {
+      if (!(dbg & 1)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -595,7 +606,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const fl
             acc[4 * qm + i][j] = mfma16(fb[j], fa[i], acc[4 * qm + i][j]);   // C^T sub-tiles
       }
       __builtin_amdgcn_s_setprio(0);
-      if (GRP == 0 && (pp & 1) && !(p.dbg & 16)) deadline((I + 2) >> 2, I, neh);
+      if (GRP == 0 && (pp & 1) && !(dbg & 16)) deadline((I + 2) >> 2, I, neh);
       stamp(5);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -603,10 +614,10 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, char* smem, const fl
     }
   }
   if constexpr (GRP == 0) __builtin_amdgcn_s_barrier();    // balance group 1's extra barrier
-  if (!(p.dbg & 2)) persist_epilogue<T, C, EPI>(p, cur, acc, bias_lds, lane, wm, wn);
+  if (!(dbg & 2)) persist_epilogue<T, C, EPI>(p, epi_item(cur), acc, bias_lds, lane, wm, wn);
 }
 
-template <typename T, bool AK, bool BK, int EPI, bool STAMP = false>
+template <typename T, bool AK, bool BK, int EPI, int MODE = 0>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* bias_lds = (float*)(smem + PP_NSLOT * PP_SLOT);
@@ -622,13 +633,9 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p) {
   }
   __syncthreads();
   if (nm <= 0 || p.K < 64) return;
-  if constexpr (STAMP) {
-    if ((threadIdx.x >> 6) < 4) pp_run<T, AK, BK, EPI, 0, true>(p, smem, bias_lds, nm, W);
-    else pp_run<T, AK, BK, EPI, 1, true>(p, smem, bias_lds, nm, W);
-  } else {
-    if ((threadIdx.x >> 6) < 4) pp_run<T, AK, BK, EPI, 0>(p, smem, bias_lds, nm, W);
-    else pp_run<T, AK, BK, EPI, 1>(p, smem, bias_lds, nm, W);
-  }
+  const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  if ((threadIdx.x >> 6) < 4) pp_run<T, AK, BK, EPI, 0, MODE>(p, lbase, smem, bias_lds, nm, W);
+  else pp_run<T, AK, BK, EPI, 1, MODE>(p, lbase, smem, bias_lds, nm, W);
 }
 
 // the persistent configuration (gemm_persist_kernel): cfg 40 = Cfg5's tile (128-B K-tiles, 2
@@ -668,8 +675,10 @@ static void launch_persist_epi(const GemmParams& p, int blocks, hipStream_t st) 
 template <typename T, bool AK, bool BK, int EPI>
 static void launch_pp_epi(const GemmParams& p, int blocks, hipStream_t st) {
   void (*fn)(GemmParams) = gemm_pp_kernel<T, AK, BK, EPI>;
-  if constexpr (EPI == 0 && sizeof(T) == 2)
-    if (p.dbg & 8) fn = gemm_pp_kernel<T, AK, BK, EPI, true>;
+  if constexpr (EPI == 0 && sizeof(T) == 2) {
+    if (p.dbg & 8) fn = gemm_pp_kernel<T, AK, BK, EPI, 2>;
+    else if (p.dbg & 55) fn = gemm_pp_kernel<T, AK, BK, EPI, 1>;
+  }
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
   int nb = 0;

@@ -907,7 +907,8 @@ def attn_backward(saved, go, dq, dk, dv):
             buf.copy_(tmp)
         return
     if (fused and ops._attn_dkdv["on"] and _small_aligned(dk, kcol, cd)
-            and _small_aligned(dv, vcol, cd)):
+            and _small_aligned(dv, vcol, cd)
+            and ops.attn_dkdv_ok(N, H, Lq, Lk, dh, so_l, sq_l, dk.stride(0), dv.stride(0))):
         # P and dS (rows of 128-key tiles) -> dK = dS^T Q and dV = P^T dO in one persistent kernel
         ldp = ops.attn_dkdv_ldp(Lk)
         P = torch.empty(N * H * Lq * ldp, dtype=cd, device=dev)

@@ -285,6 +285,18 @@ def attn_dkdv_ldp(Lk: int) -> int:
     return (Lk + 127) // 128 * 128
 
 
+def attn_dkdv_ok(N, H, Lq, Lk, dh, sgo_l, sq_l, sdk_l, sdv_l) -> bool:
+    """Host-side mirror of jmt_attn_dkdv's range checks (csrc/attn_dkdv.hip): 512-wide heads,
+    32-bit row offsets of dO / Q / P (Lq rows < 2 GiB) and of a 128-row dK / dV tile, and the
+    item count.  The caller takes the batched-GEMM dK / dV path when this says no."""
+    ldp = attn_dkdv_ldp(Lk)
+    lim = 1 << 31
+    return (dh == 512 and sdk_l >= H * dh and sdv_l >= H * dh
+            and 128 * sdk_l * 2 < lim and 128 * sdv_l * 2 < lim
+            and N * H * 2 * (ldp // 128) < lim
+            and Lq * sgo_l * 2 < lim and Lq * sq_l * 2 < lim and Lq * ldp * 2 < lim)
+
+
 def attn_dkdv(dtype, N, H, Lq, Lk, dh, p, ds, ldp, go_ptr, sgo, q_ptr, sq, dk_ptr, sdk, dv_ptr,
               sdv):
     """dV = P^T dO and dK = dS^T Q per (n, h) from attn_bwd's P / dS (ldp >= attn_dkdv_ldp(Lk));

@@ -8,6 +8,7 @@ Parameters that never receive a gradient (the reference's unused `final_encoder`
 so `used_parameters()` finds them with one probe backward."""
 from __future__ import annotations
 
+import os
 from typing import Iterable, List, Optional
 
 import torch
@@ -17,6 +18,10 @@ from . import functional as F
 from . import ops
 
 
+def _bump_grad_gen(_p):
+    F._grad_gen[0] += 1
+
+
 class FusedSGD:
     def __init__(self, params: Iterable[torch.nn.Parameter], lr: float, momentum: float = 0.0,
                  dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
@@ -24,7 +29,15 @@ class FusedSGD:
         """fuse_zero_grad: the step kernel zeroes each gradient after reading it (jmt_sgd_step_zero)
         and the next zero_grad() issues nothing while no gradient has been written since — the
         training step of train.py:96-315 without a fill launch.  Off by default: torch's
-        optimizer.step() leaves .grad readable until zero_grad()."""
+        optimizer.step() leaves .grad readable until zero_grad().
+
+        Contract of the skipped fill: "written since" is known from functional._grad_gen, which
+        the HIP gradient writers (functional._grad_buffer) and torch autograd's accumulation into
+        .grad (post-accumulate hooks) bump.  Anything else that writes into a .grad in place
+        (p.grad.add_/copy_ by hand, a helper writing into the flat views) is invisible to it and
+        the next backward would add onto the stale values: call zero_grad(force=True) after such
+        a write, or set JMT_CHECK_ZERO_GRAD=1 to have every skipped fill verify (one reduction +
+        host sync) that the gradients are in fact zero."""
         self.params: List[torch.nn.Parameter] = list(params)
         assert self.params, "no parameters"
         dev = self.params[0].device
@@ -64,20 +77,38 @@ class FusedSGD:
         # zeroing step (functional._grad_gen counts the HIP writers; torch autograd accumulation
         # into .grad is caught by the post-accumulate hooks)
         self._clean_gen = F._grad_gen[0]
-        for p in self.params:
-            p.register_post_accumulate_grad_hook(lambda _p: F._grad_gen.__setitem__(
-                0, F._grad_gen[0] + 1))
+        self._hooks = [p.register_post_accumulate_grad_hook(_bump_grad_gen) for p in self.params]
 
-    def zero_grad(self, set_to_none: bool = False):
+    def close(self):
+        """Remove the gradient-write hooks this optimizer put on its parameters (also on garbage
+        collection); the parameters keep their flat-buffer storage."""
+        for h in getattr(self, "_hooks", ()):
+            h.remove()
+        self._hooks = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def zero_grad(self, set_to_none: bool = False, force: bool = False):
         """optimizer.zero_grad().  With fuse_zero_grad the step kernel already zeroed the
-        gradients, so after a step (and no gradient write since) this issues nothing."""
+        gradients, so after a step (and no gradient write since) this issues nothing; force=True
+        fills regardless (after an in-place .grad write the write counter cannot see)."""
         for p, g in zip(self.params, self._gviews):
             if p.grad is None or p.grad.data_ptr() != g.data_ptr():
                 p.grad = g
                 self._clean_gen = None
-        if not self.fuse_zero_grad or self._clean_gen != F._grad_gen[0]:
+        if force or not self.fuse_zero_grad or self._clean_gen != F._grad_gen[0]:
             self.flat_g.zero_()
             self._clean_gen = F._grad_gen[0]
+        elif os.environ.get("JMT_CHECK_ZERO_GRAD", "0") == "1":
+            nz = int(torch.count_nonzero(self.flat_g))
+            if nz:
+                raise RuntimeError(f"FusedSGD.zero_grad: {nz} gradient element(s) written outside "
+                                   "the tracked writers since the fused zeroing step (see the "
+                                   "fuse_zero_grad contract); call zero_grad(force=True)")
 
     @torch.no_grad()
     def step_amp(self, amp_state: torch.Tensor):
@@ -85,7 +116,8 @@ class FusedSGD:
         the momentum buffer is initialised is then decided on the device (steps_taken), so plain
         step() calls cannot follow scaled ones."""
         self._amp = True
-        _lib.call("jmt_sgd_step_amp_zero" if self.fuse_zero_grad else "jmt_sgd_step_amp", self.numel, self.flat_p.data_ptr(), self.flat_g.data_ptr(),
+        fn = "jmt_sgd_step_amp_zero" if self.fuse_zero_grad else "jmt_sgd_step_amp"
+        _lib.call(fn, self.numel, self.flat_p.data_ptr(), self.flat_g.data_ptr(),
                   self.buf.data_ptr() if self.buf is not None else None, self.lr, self.momentum,
                   self.dampening, self.weight_decay, int(self.nesterov), int(self.first),
                   amp_state.data_ptr(),

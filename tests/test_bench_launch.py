@@ -106,3 +106,39 @@ def test_bench_gpus2_gloo_on_one_gpu():
     assert j["config"]["global_batch"] == 8
     assert j["parity"]["pass"], j["parity"]
     assert "[rank 0] rank 0/2" in r.stderr and "[rank 1] rank 1/2" in r.stderr
+
+
+class _Ev:
+    def __init__(self, t):
+        self.t = t
+
+    def elapsed_time(self, other):
+        return other.t - self.t
+
+
+def _probe_with(seq_per_step):
+    b = _bench()
+    pr = b.FamilyProbe()
+    for step, seq in enumerate(seq_per_step):
+        for fam, ms in seq:
+            pr.rec.append((fam, 1e9, None, (_Ev(0.0), _Ev(ms))))
+            pr.cal.append(((_Ev(0.0), _Ev(0.010)), (_Ev(0.0), _Ev(0.020))))
+    return pr
+
+
+def test_family_probe_per_position_medians_need_identical_sequences():
+    """the per-position medians are taken only when every probe step issued the same
+    (family, flops) sequence; a different sequence with the same length falls back to the
+    per-launch sum (flagged in the summary)."""
+    same = [[("gemm_nt", 0.1), ("gemm_nn", 0.2)]] * 3
+    s = _probe_with(same).summary(3)
+    assert s["per_position_medians"] is True
+    fam = {f["family"]: f for f in s["families"]}
+    assert fam["gemm_nt"]["launches_per_step"] == 1 and fam["gemm_nn"]["launches_per_step"] == 1
+    diff = [[("gemm_nt", 0.1), ("gemm_nn", 0.2)], [("gemm_nn", 0.2), ("gemm_nt", 0.1)],
+            [("gemm_nt", 0.1), ("gemm_nn", 0.2)]]
+    s = _probe_with(diff).summary(3)
+    assert s["per_position_medians"] is False
+    fam = {f["family"]: f for f in s["families"]}
+    assert fam["gemm_nt"]["launches_per_step"] == 1 and fam["gemm_nn"]["launches_per_step"] == 1
+    assert abs(fam["gemm_nn"]["avg_launch_us_raw"] - 200.0) < 1e-6

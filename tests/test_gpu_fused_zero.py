@@ -107,6 +107,30 @@ def test_fused_sgd_zero_grad_on_off_three_steps_bit_identical():
         assert torch.equal(pa, pb) and torch.equal(ba, bb)
 
 
+def test_fused_sgd_untracked_grad_write_check_force_and_close(monkeypatch):
+    """The skipped fill's contract: an in-place .grad write outside the tracked writers is caught
+    by JMT_CHECK_ZERO_GRAD=1, zero_grad(force=True) clears it, close() removes the hooks."""
+    from models.fc_layer import FcLayer
+    m = FcLayer(32, 16).to(DEV)
+    opt = FusedSGD(list(m.parameters()), **SGD_KW, fuse_zero_grad=True)
+    x = torch.randn(8, 32, device=DEV)
+    with JF.compute_mode(torch.float32):
+        (m(x) ** 2).mean().backward()
+    opt.step()
+    assert int(torch.count_nonzero(opt.flat_g)) == 0
+    m.fc_layer.weight.grad.add_(1.0)                    # untracked write
+    monkeypatch.setenv("JMT_CHECK_ZERO_GRAD", "1")
+    with pytest.raises(RuntimeError, match="outside the tracked writers"):
+        opt.zero_grad()
+    opt.zero_grad(force=True)
+    assert int(torch.count_nonzero(opt.flat_g)) == 0
+    opt.zero_grad()                                     # clean: the check passes
+    n_hooks = len(opt._hooks)
+    assert n_hooks == len(opt.params)
+    opt.close()
+    assert opt._hooks == []
+
+
 @pytest.mark.parametrize("add_shape", [(), (1,)])
 def test_ccc_finish_add_bit_identical(add_shape):
     """CCCLoss.forward_add(x2, y2, l1) == l1 + CCCLoss(x2, y2) bit for bit (one fp32 add either

@@ -662,6 +662,43 @@ def test_attention_backward_dkdv_matches_gemm_path(Lq, Lk, N):
     assert err <= 2 * 2.0 ** -8 * ref.abs().max().item(), err
 
 
+def test_attention_backward_dkdv_out_of_range_stride_takes_gemm_path():
+    """a dK / dV row stride beyond jmt_attn_dkdv's 32-bit tile offsets (128 rows x
+    stride x 2 B >= 2 GiB) is caught by ops.attn_dkdv_ok and the backward takes the batched-GEMM
+    dK / dV path (bit-identical to JMT_ATTN_DKDV=0) instead of raising."""
+    from jmt import functional as F
+    cd = torch.bfloat16
+    E, H, N, Lq, Lk = 512, 1, 1, 70, 129
+    sl = (1 << 23) + 1024                       # 128 * sl * 2 B > 2 GiB
+    assert not ops.attn_dkdv_ok(N, H, Lq, Lk, E, 3 * E, 3 * E, sl, sl)
+    assert ops.attn_dkdv_ok(N, H, Lq, Lk, E, 3 * E, 3 * E, 2 * E, 2 * E)
+    g = torch.Generator(device=DEV).manual_seed(33)
+    qkv = torch.randn(N, Lq, 3 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    kv = torch.randn(N, Lk, 2 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    F.set_compute_dtype(cd)
+    try:
+        o, saved = F.attn_forward(qkv, kv, kv, E, H, 0, 0, E)
+    finally:
+        F.set_compute_dtype(None)
+    go = torch.randn(Lq, N, E, device=DEV, generator=g).to(cd)
+    big = torch.zeros((Lk - 1) * sl + 2 * E, device=DEV, dtype=cd)
+    res = []
+    for on in (True, False):
+        ops._attn_dkdv["on"] = on
+        try:
+            dq = torch.zeros(N, Lq, 3 * E, device=DEV, dtype=cd).permute(1, 0, 2)
+            big.zero_()
+            dkv = big.as_strided((Lk, N, 2 * E), (sl, sl * Lk, 1))
+            F.attn_backward(saved, go, dq, dkv, dkv)
+            torch.cuda.synchronize()
+            res.append((dq.float().clone(), dkv.float().clone()))
+        finally:
+            ops._attn_dkdv["on"] = True
+    del big
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert res[0][1].abs().max().item() > 0
+
+
 def test_fused_attention_forced_rescale():
     """The lazy-rescale branch of the forward (a row max rising > 8 log2 units after the first
     tile) must be exact: one key in the third 64-key tile is spiked to dominate one query row
