@@ -721,8 +721,27 @@ static int occupancy_override(int ak, int bk, int M, int N, int K, int batch, in
   return 0;
 }
 
+static int pp_split_env() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("JMT_GEMM_PPSPLIT");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
 static void plan(int dt, int M, int N, int K, int batch, int fixed_splits, int& cfg, int& splits) {
   const int bke = 128 / dtype_size(dt);
+  // few 256 x 256 tiles over a long K (the weight gradients): the split-K ping-pong kernel,
+  // one (tile, split) item per CU (gemm_persist.hip cfg 44)
+  if (fixed_splits <= 0 && pp_split_env()) {
+    const int s = pp_split_plan(dt, M, N, K, batch);
+    if (s) {
+      cfg = 44;
+      splits = s;
+      return;
+    }
+  }
   const TileModel* ms = dt == JMT_F32 ? kModels32 : kModels16;
   const int nm = dt == JMT_F32 ? 1 : 2;
   double best = 1e300;
@@ -891,6 +910,11 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
       return JMT_OK;
     }
   }
+  // split-K ping-pong (cfg 44): forced, or where the planner's split count came from it
+  const bool pp_split = splits > 1 && pp_split_ok(dt, d->M, d->N, d->K, splits) &&
+                        (cfg == 44 || (cfg == 0 && pp_split_env() &&
+                                       pp_split_plan(dt, d->M, d->N, d->K, batch0 * batch1)));
+  if (cfg == 44) cfg = 0;
   if (cfg == 40 || cfg == 43) cfg = 5;      // persistent configs not applicable: same tile
   if (dt == JMT_F32 && cfg >= 10) cfg = 1;   // occupancy / 160-row configs: 16-bit only
   if (cfg == 32 && !d->a_kmajor) cfg = 5;    // 160-row tile: K-major A only
@@ -908,16 +932,25 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   // 256x256 tile does not and runs the split-K qkv / FFN wgrad shapes at least as fast
   // (profiles/r03_wgrad_dbias.jsonl)
   if (d->n_dbias > 0 && cfg == 10) cfg = 5;
-  int bm, bn;
-  cfg_tile(cfg, bm, bn);
-  p.tiles_m = (d->M + bm - 1) / bm;
-  p.tiles_n = (d->N + bn - 1) / bn;
   hipStream_t st = as_stream(stream);
-  dim3 grid(p.tiles_m * p.tiles_n, batch0 * batch1, splits);
-  if (dt == JMT_F32) launch_t<float>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
-  else if (dt == JMT_BF16) launch_t<__bf16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
-  else launch_t<_Float16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
-  JMT_LAUNCH_CHECK("jmt_gemm");
+  if (pp_split) {
+    p.tiles_m = d->M / 256;
+    p.tiles_n = d->N / 256;
+    const int W = p.tiles_m * p.tiles_n * batch0 * batch1 * splits;
+    const int ncu = num_cus_persist();
+    launch_gemm_pp_split(p, dt, d->a_kmajor, d->b_kmajor, d->n_dbias > 0, W < ncu ? W : ncu, st);
+    JMT_LAUNCH_CHECK("jmt_gemm(split-K ping-pong)");
+  } else {
+    int bm, bn;
+    cfg_tile(cfg, bm, bn);
+    p.tiles_m = (d->M + bm - 1) / bm;
+    p.tiles_n = (d->N + bn - 1) / bn;
+    dim3 grid(p.tiles_m * p.tiles_n, batch0 * batch1, splits);
+    if (dt == JMT_F32) launch_t<float>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
+    else if (dt == JMT_BF16) launch_t<__bf16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
+    else launch_t<_Float16>(p, d->a_kmajor, d->b_kmajor, cfg, grid, st);
+    JMT_LAUNCH_CHECK("jmt_gemm");
+  }
   if (splits > 1) {
     const bool v4 = d->N % 4 == 0 && p.c_vec4;
     const int64_t total = (int64_t)d->M * d->N * batch0 * batch1 / (v4 ? 4 : 1);

@@ -38,6 +38,7 @@ __device__ __forceinline__ void wait_young(int k, bool st) {
 
 struct PItem {
   int m0, n0, b0, b1;
+  int sp, kt0, len;             // split-K: split index, its first K-tile (64 deep) and count
 };
 
 // work item w (block w % G, G a multiple of 8: the hardware deals blocks to the XCDs round-robin)
@@ -56,7 +57,76 @@ __device__ __forceinline__ PItem pitem(const GemmParams& p, int w, int W) {
   return it;
 }
 
-// EPI: 0 plain, 1 beta * C, 2 ReLU mask (aux), 3 both — compile-time, so that every load the
+// pitem for w, w + G, w + 2 G, ... without divisions per item: G is a multiple of 8, so w's XCD
+// slot x is fixed and the logical tile index L advances by G / 8 = dm * tiles_n + dn
+// With split-K (p.splits = S > 1, the ping-pong kernel only) the split index is the fastest
+// batch coordinate: the tiles of one (batch, split) — which share that K range's A and B panels —
+// are consecutive logical items, so they run together on one XCD's L2.
+struct PWalk {
+  int mt, nt, b0, b1, sp;
+  int dm, dn;
+};
+__device__ __forceinline__ PWalk pwalk_init(const GemmParams& p, int w, int W, int G) {
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int x = w & 7, q = W >> 3, r = W & 7;
+  const int L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (w >> 3);
+  const int bs = L / ntile, t = L - bs * ntile;
+  const int b = bs / p.splits;
+  PWalk s;
+  s.sp = bs - b * p.splits;
+  s.mt = t / p.tiles_n;
+  s.nt = t - s.mt * p.tiles_n;
+  s.b0 = b / p.batch1;
+  s.b1 = b - s.b0 * p.batch1;
+  s.dm = (G >> 3) / p.tiles_n;
+  s.dn = (G >> 3) - s.dm * p.tiles_n;
+  return s;
+}
+__device__ __forceinline__ void pwalk_next(const GemmParams& p, PWalk& s) {
+  s.nt += s.dn;
+  s.mt += s.dm;
+  if (s.nt >= p.tiles_n) {
+    s.nt -= p.tiles_n;
+    ++s.mt;
+  }
+  while (s.mt >= p.tiles_m) {
+    s.mt -= p.tiles_m;
+    if (++s.sp == p.splits) {
+      s.sp = 0;
+      if (++s.b1 == p.batch1) {
+        s.b1 = 0;
+        ++s.b0;
+      }
+    }
+  }
+}
+__device__ __forceinline__ PItem pwalk_item(const GemmParams& p, const PWalk& s) {
+  PItem it;
+  it.m0 = s.mt * 256;
+  it.n0 = s.nt * 256;
+  it.b0 = s.b0;
+  it.b1 = s.b1;
+  it.sp = s.sp;
+  const int nkt = p.K >> 6;                 // split sp: K-tiles [sp nkt / S, (sp + 1) nkt / S)
+  if (p.splits == 1) {
+    it.kt0 = 0;
+    it.len = nkt;
+  } else {
+    it.kt0 = s.sp * nkt / p.splits;
+    it.len = (s.sp + 1) * nkt / p.splits - it.kt0;
+  }
+  return it;
+}
+
+// two floats -> two 16-bit values in one dword (one v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32, RNE)
+template <typename T>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{a, b}, t2));
+}
+
+// EPI: 0 plain, 1 beta * C, 2 ReLU mask (aux), 3 both, 4 plain + ReLU — compile-time, so that every load the
 // epilogue issues is consumed on every path (a conditional load left hipcc unsure at the loop
 // head and it waited vmcnt(4) there, draining the next K-tile's DMA every iteration)
 // rows I0 .. I0 + NI - 1 of the wave's sub-tiles (the ping-pong kernel stores its two 64-row
@@ -64,7 +134,8 @@ __device__ __forceinline__ PItem pitem(const GemmParams& p, int w, int W) {
 template <typename T, class C, int EPI, int I0 = 0, int NI = C::TM>
 __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PItem& it,
                                                  f32x4 (&acc)[C::TM][C::TN],
-                                                 const float* bias_lds, int lane, int wm, int wn) {
+                                                 const float* bias_lds, int lane, int wm, int wn,
+                                                 bool nostore = false) {
   static_assert(C::TN % 2 == 0, "paired stores");
   T* cp;
   int64_t cbase;
@@ -107,7 +178,8 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
       for (int e = 0; e < 4; ++e) bias4[j][e] = 0.f;
   }
   const float alpha = p.alpha, beta = p.beta;
-  const bool relu = p.relu != 0;
+  // ReLU: compile-time for the plain forms (EPI 0 / 4), a runtime flag with beta * C / the mask
+  const bool relu = EPI == 4 || ((EPI & 3) != 0 && p.relu != 0);
   const T* auxp = (const T*)p.aux;
   // beta * C and the ReLU-backward mask (aux > 0) of the one-block-per-tile epilogue, in its
   // order (+ beta C, ReLU, mask); their 8-B loads of row i + 1 are in flight while row i is
@@ -126,12 +198,15 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
     }
   };
   if constexpr (ldc_ || lda_) load_row(I0, cr[I0 & 1], ar[I0 & 1]);
+  // the lane's store address for sub-tile row 0, sub-tile pair 0: row rl, its 8-column chunk
+  T* const cl = cp + cbase + (int64_t)(it.m0 + wm * C::WTM + rl) * p.ldc + it.n0 + wn * C::WTN +
+                16 * (g & 1) + 8 * (g >> 1);
 #pragma unroll
   for (int i = I0; i < I0 + NI; ++i) {
-    const int m = it.m0 + wm * C::WTM + 16 * i + rl;
-    const int64_t rowo = cbase + (int64_t)m * p.ldc;
     if constexpr (ldc_ || lda_)
       if (i + 1 < I0 + NI) load_row(i + 1, cr[(i + 1) & 1], ar[(i + 1) & 1]);
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 vj[C::TN / 2];
 #pragma unroll
     for (int jp = 0; jp < C::TN / 2; ++jp) {
       uint32_t pk[2][2];
@@ -151,29 +226,60 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
             if constexpr (lda_)
               if (!(to_f(av[e]) > 0.f)) x[e] = 0.f;
           }
-        } else if (relu) {
+        } else if (EPI == 4) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) x[e] = fmaxf(x[e], 0.f);
         }
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          T hh[2] = {from_f<T>(x[2 * q]), from_f<T>(x[2 * q + 1])};
-          pk[h][q] = *(const uint32_t*)hh;
-        }
+        for (int q = 0; q < 2; ++q) pk[h][q] = pack2<T>(x[2 * q], x[2 * q + 1]);
       }
       const auto r0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
       const auto r1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
-      const int n = it.n0 + wn * C::WTN + 16 * (2 * jp + (g & 1)) + 8 * (g >> 1);
-      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
-      JMT_DCHECK(m < p.M && n + 8 <= p.N);
-#ifdef JMT_EPI_PLAIN
-      *(u32x4*)(cp + rowo + n) = v;
-#else
-      __builtin_nontemporal_store(v, (u32x4*)(cp + rowo + n));
-#endif
+      vj[jp] = u32x4{r0[0], r1[0], r0[1], r1[1]};
+    }
+    if (nostore) continue;
+    T* const crow = cl + (int64_t)(16 * i) * p.ldc;
+#pragma unroll
+    for (int jp = 0; jp < C::TN / 2; ++jp) {
+      JMT_DCHECK(it.m0 + wm * C::WTM + 16 * i + rl < p.M &&
+                 it.n0 + wn * C::WTN + 32 * jp + 16 * (g & 1) + 8 * (g >> 1) + 8 <= p.N);
+      __builtin_nontemporal_store(vj[jp], (u32x4*)(crow + 32 * jp));
     }
   }
+}
+
+// split-K form of the epilogue (ping-pong kernel, p.splits > 1): rows I0 .. I0 + NI - 1 of the
+// wave's sub-tiles as raw fp32 partial sums into the item's slab, ws[(sp nb + b) M + m][n] (the
+// layout splitk_reduce_kernel sums in split order): one 16-B store per sub-tile and lane
+template <class C, int I0, int NI>
+__device__ __forceinline__ void pp_slab_epilogue(const GemmParams& p, const PItem& it,
+                                                 const f32x4 (&acc)[C::TM][C::TN], int lane,
+                                                 int wm, int wn) {
+  const int g = lane >> 4, rl = lane & 15;
+  const int nb = p.batch0 * p.batch1;
+  const int b = it.b0 * p.batch1 + it.b1;
+  float* const sl = p.ws + ((int64_t)it.sp * nb + b) * (int64_t)p.M * p.N +
+                    (int64_t)(it.m0 + wm * C::WTM + rl) * p.N + it.n0 + wn * C::WTN + 4 * g;
+#pragma unroll
+  for (int i = I0; i < I0 + NI; ++i) {
+    float* const row = sl + (int64_t)(16 * i) * p.N;
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) __builtin_nontemporal_store(acc[i][j], (f32x4*)(row + 16 * j));
+  }
+}
+
+// the A row sums of one 16-row sub-tile (lane group g = lane >> 4 holds k-slices of row
+// lane & 15) into the item's split partial, dbias_ws[(sp nb + b) M + m]: ONE store instruction
+// (lanes 0-15), issued on every path so the epilogue's VMEM count stays exact.  The N tiles of
+// one row panel store the same sums (same fragments, same order): identical bits.
+__device__ __forceinline__ void pp_rowsum_store(const GemmParams& p, const PItem& it, float v,
+                                                int row0, int lane) {
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  const int nb = p.batch0 * p.batch1;
+  const int b = it.b0 * p.batch1 + it.b1;
+  float* const d = p.dbias_ws + ((int64_t)it.sp * nb + b) * p.M + it.m0 + row0 + (lane & 15);
+  if (lane < 16) *d = v;
 }
 
 // ABL: development ablation (compute_tile MODE; dbg 64 -> 1, 128 -> 2), bf16 plain epilogue only
@@ -230,12 +336,16 @@ void gemm_persist_kernel(GemmParams p) {
   };
   // issue cursor: the next K-tile (stream index t) whose DMA goes out
   int iss_kt = 0, iss_k = 0;
-  PItem iss = pitem(p, blockIdx.x, W);
+  PWalk iss_w = pwalk_init(p, blockIdx.x, W, G);
+  PItem iss = pwalk_item(p, iss_w);
   auto advance_issue = [&]() {
     if (++iss_kt == nkt) {
       iss_kt = 0;
       ++iss_k;
-      if (iss_k < nm) iss = pitem(p, blockIdx.x + iss_k * G, W);
+      if (iss_k < nm) {
+        pwalk_next(p, iss_w);
+        iss = pwalk_item(p, iss_w);
+      }
     }
   };
 #pragma unroll
@@ -257,7 +367,8 @@ void gemm_persist_kernel(GemmParams p) {
   for (int i = 0; i < C::TM; ++i)
 #pragma unroll
     for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  PItem cur = pitem(p, blockIdx.x, W);
+  PWalk cur_w = pwalk_init(p, blockIdx.x, W, G);
+  PItem cur = pwalk_item(p, cur_w);
   int cur_k = 0, cur_kt = 0;
   int last_ep = -(1 << 20);
   // dbg 32: wait for the stores as well (A/B of the overlap); dbg 2 issues no stores
@@ -310,7 +421,10 @@ void gemm_persist_kernel(GemmParams p) {
         for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       last_ep = s;
       cur_kt = 0;
-      if (++cur_k < nm) cur = pitem(p, blockIdx.x + cur_k * G, W);
+      if (++cur_k < nm) {
+        pwalk_next(p, cur_w);
+        cur = pwalk_item(p, cur_w);
+      }
     }
   }
 }
@@ -376,15 +490,19 @@ __device__ __forceinline__ void wait_vm_le(int n) {
 // development: s_memtime stamps of one block's segments (dbg 8, bf16 EPI 0 only; read with
 // jmt_gemm_pp_stamps_read): [wave][K-tile < PP_STK][phase][6]
 constexpr int PP_STK = 24;
-__device__ uint64_t g_pp_stamps[8 * PP_STK * 4 * 6];
+__device__ uint64_t g_pp_stamps[8 * PP_STK * 4 * 8];
 
-template <typename T, bool AK, bool BK, int EPI, int GRP, int MODE = 0>
+// SPL: 0 the 16-bit C epilogue (persist_epilogue, EPI), 1 split-K fp32 slabs (pp_slab_epilogue),
+// 2 slabs + the A row sums (dbias_ws)
+template <typename T, bool AK, bool BK, int EPI, int GRP, int MODE = 0, int SPL = 0>
 __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, const char* smem,
                                        const float* bias_lds, int nm, int W) {
   using C = CfgPP;
   typedef typename Frag16<T>::t F;
-  constexpr int NST = C::TM * (C::TN / 2);                 // epilogue stores per wave
-  constexpr int NLD = ((EPI & 1) ? C::TM * C::TN : 0) + ((EPI & 2) ? C::TM * C::TN : 0);
+  // epilogue VMEM operations per wave: 16-B stores of paired 16-bit sub-tiles, or of fp32
+  // sub-tiles (+ one row-sum store per half), and the beta * C / mask loads
+  constexpr int NST = SPL ? C::TM * C::TN + (SPL == 2 ? 2 : 0) : C::TM * (C::TN / 2);
+  constexpr int NLD = SPL ? 0 : ((EPI & 1) ? C::TM * C::TN : 0) + ((EPI & 2) ? C::TM * C::TN : 0);
   constexpr int SUB = (GRP + PP_D) & 1;                    // parity of this group's pieces
   // VMEM operations younger than the wave's last piece of k-half g at its deadline, away from
   // the stream's end: its pieces of the load intervals (4g + 2 + SUB - PP_D, 4g - 2 + GRP]
@@ -400,8 +518,16 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
   const int dbg = MODE ? p.dbg : 0;
   const int wn = wl;
   const int G = gridDim.x;
-  const int nkt = p.K / 64;
-  const int nT = nm * nkt;
+  // K-tiles of this block's items (split-K items differ by one K-tile at most)
+  int nT = nm * (p.K >> 6);
+  if (SPL && p.splits > 1) {
+    PWalk w = pwalk_init(p, blockIdx.x, W, G);
+    nT = 0;
+    for (int k = 0; k < nm; ++k) {
+      if (k) pwalk_next(p, w);
+      nT += pwalk_item(p, w).len;
+    }
+  }
   const int npieces = 8 * nT;
   const int ins0 = SUB * 8 + 2 * wl;
 
@@ -423,12 +549,13 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
   const int segb = p.b_mode == 2 ? p.b_kseg / 64 : 1 << 30;
 
   // the issue stream: item iss_k, K-tile iss_kt of it, per-lane sources pa / pb of that K-tile
-  PItem iss_it = pitem(p, blockIdx.x, W);
+  PWalk iss_w = pwalk_init(p, blockIdx.x, W, G);
+  PItem iss_it = pwalk_item(p, iss_w);
   int iss_k = 0, iss_kt = 0, lefta = 0, leftb = 0;
   const char* pa[2];
   const char* pb[2];
   auto set_stream = [&]() {
-    const int k0 = iss_kt * 64;
+    const int k0 = (iss_it.kt0 + iss_kt) * 64;
     int ka, kb;
     const T* A = operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, iss_it.b0, iss_it.b1,
                                  p.a_kseg, k0, ka);
@@ -447,10 +574,11 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
     leftb = segb - (kb >> 6);
   };
   auto next_ktile = [&]() {
-    if (++iss_kt == nkt) {
+    if (++iss_kt == iss_it.len) {
       iss_kt = 0;
       if (++iss_k < nm) {
-        iss_it = pitem(p, blockIdx.x + iss_k * G, W);
+        pwalk_next(p, iss_w);
+        iss_it = pwalk_item(p, iss_w);
         set_stream();
       }
     } else if (--lefta == 0 || --leftb == 0) {
@@ -512,20 +640,31 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
 #pragma unroll
     for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   F fa[4], fb[4];
-  PItem cur = pitem(p, blockIdx.x, W);
-  int cur_k = 0, cur_left = nkt;
+  PWalk cur_w = pwalk_init(p, blockIdx.x, W, G);
+  PItem cur = pwalk_item(p, cur_w);
+  int cur_left = cur.len;
+  float rsum[2] = {0.f, 0.f};                              // SPL 2: row sums of qm 0 / 1
   // epilogue of an item in two halves: rows 0-63 of the wave (quadrant qm = 0, final after
   // phase 2 of the item's last K-tile) in that K-tile's phase-3 load segment, rows 64-127 in the
   // next K-tile's phase-0 load segment — half the store burst per segment
   bool epA = false, epB = false;
 
-  const bool stamping = STAMP && blockIdx.x == 0 && lane == 0;
-  // ablation dbg 32: every epilogue stores to tile (0, 0) of batch 0 (L2-resident C)
-  auto epi_item = [&](const PItem& it) {
-    PItem e = it;
-    if (dbg & 32) e.m0 = e.n0 = e.b0 = e.b1 = 0;
-    return e;
+  // the stores of one epilogue half (h = 0: rows 0-63 of the wave, 1: rows 64-127) of item cur
+  auto epilogue_half = [&](int h) {
+    if constexpr (SPL) {
+      if (h == 0) pp_slab_epilogue<C, 0, 4>(p, cur, acc, lane, wm, wn);
+      else pp_slab_epilogue<C, 4, 4>(p, cur, acc, lane, wm, wn);
+      if constexpr (SPL == 2) {                            // this wave's sub-tile (qm h, i wn)
+        pp_rowsum_store(p, cur, rsum[h], wm * C::WTM + 64 * h + 16 * wn, lane);
+        rsum[h] = 0.f;
+      }
+    } else {
+      if (h == 0) persist_epilogue<T, C, EPI, 0, 4>(p, cur, acc, bias_lds, lane, wm, wn, dbg & 64);
+      else persist_epilogue<T, C, EPI, 4, 4>(p, cur, acc, bias_lds, lane, wm, wn, dbg & 64);
+    }
   };
+
+  const bool stamping = STAMP && blockIdx.x == 0 && lane == 0;
   for (int t = 0; t < nT; ++t) {
 #pragma unroll
     for (int pp = 0; pp < 4; ++pp) {
@@ -534,7 +673,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
       auto stamp = [&](int e) {
         if constexpr (STAMP) {
           if (stamping && t < PP_STK)
-            g_pp_stamps[((wid * PP_STK + t) * 4 + pp) * 6 + e] = __builtin_amdgcn_s_memtime();
+            g_pp_stamps[((wid * PP_STK + t) * 4 + pp) * 8 + e] = __builtin_amdgcn_s_memtime();
         }
       };
       stamp(0);
@@ -542,27 +681,29 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
       if (pp == 0) {
         epB = false;
         if (cur_left == 0) {                               // previous item done: rows 64-127
-          if (!(dbg & 2))
-            persist_epilogue<T, C, EPI, 4, 4>(p, epi_item(cur), acc, bias_lds, lane, wm, wn);
-#pragma unroll
-          for (int i = 4; i < C::TM; ++i)
-#pragma unroll
-            for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          cur = pitem(p, blockIdx.x + (++cur_k) * G, W);
-          cur_left = nkt;
+          if (!(dbg & 2)) epilogue_half(1);
+          pwalk_next(p, cur_w);
+          cur = pwalk_item(p, cur_w);
+          cur_left = cur.len;
           epB = true;
         }
         --cur_left;
         epA = false;
       }
       if (pp == 3 && cur_left == 0 && t + 1 < nT) {        // the item's last K-tile: rows 0-63
-        if (!(dbg & 2)) persist_epilogue<T, C, EPI, 0, 4>(p, epi_item(cur), acc, bias_lds, lane, wm, wn);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!(dbg & 2)) epilogue_half(0);
         epA = true;
       }
+      // piece P = I + PP_D: K-tile t + (L >> 3), k-half 2 (t + (L >> 3)) + ((L >> 2) & 1),
+      // quarter L & 3, L = 2 pp + GRP + PP_D (compile-time after unrolling).  The stream's K-tile
+      // step comes before this segment's LDS reads: an item switch waits lgkmcnt(0) for its
+      // scalar loads, which would otherwise also wait for the reads in flight
+      stamp(6);
+      const int L = 2 * pp + GRP + PP_D;
+      const int Lp = 2 * pp - 2 + GRP + PP_D;
+      if (pp > 0 ? ((L >> 3) != (Lp >> 3)) : ((L >> 3) != ((L + 6) >> 3) - 1))
+        next_ktile();
+      stamp(7);
       const char* slot = smem + ((2 * t + ks) & (PP_NSLOT - 1)) * PP_SLOT;
       if (qm == 0) {
 #pragma unroll
@@ -573,15 +714,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
       for (int i = 0; i < 4; ++i)
         fa[i] = read_frag16<T, AK, 64, 256>(slot, wm * C::WTM + 64 * qm + 16 * i, 0);
       stamp(1);
-      {
-        // piece P = I + PP_D: K-tile t + (L >> 3), k-half 2 (t + (L >> 3)) + ((L >> 2) & 1),
-        // quarter L & 3, L = 2 pp + GRP + PP_D (compile-time)
-        const int L = 2 * pp + GRP + PP_D;
-        const int Lp = 2 * pp - 2 + GRP + PP_D;
-        if (pp > 0 ? ((L >> 3) != (Lp >> 3)) : ((L >> 3) != ((L + 6) >> 3) - 1))
-          next_ktile();
-        if (!(dbg & 4) && I + PP_D < npieces) issue(2 * (t + (L >> 3)) + ((L >> 2) & 1), L & 3);
-      }
+      if (!(dbg & 4) && I + PP_D < npieces) issue(2 * (t + (L >> 3)) + ((L >> 2) & 1), L & 3);
       stamp(2);
       // epilogue halves younger than the wave's last piece of the k-half due (a segment issues
       // its epilogue half BEFORE its piece; counting one too many would under-wait): at phase 1
@@ -606,6 +739,28 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
             acc[4 * qm + i][j] = mfma16(fb[j], fa[i], acc[4 * qm + i][j]);   // C^T sub-tiles
       }
       __builtin_amdgcn_s_setprio(0);
+      if constexpr (SPL == 2) {
+        // A row sums of the wave's sub-tile (qm, i = wn), from the fragment the MFMAs just read
+        const float r = rsum[qm];
+        if (wn == 0) rsum[qm] = rowsum8(fa[0], r);
+        else if (wn == 1) rsum[qm] = rowsum8(fa[1], r);
+        else if (wn == 2) rsum[qm] = rowsum8(fa[2], r);
+        else rsum[qm] = rowsum8(fa[3], r);
+      }
+      // rows stored by this phase's load segment restart at 0, here behind the MFMAs that do not
+      // touch them (rows 0-63 after phase 3's epilogue half, rows 64-127 after phase 0's)
+      if (pp == 3 && epA) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (pp == 0 && epB) {
+#pragma unroll
+        for (int i = 4; i < C::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
       if (GRP == 0 && (pp & 1) && !(dbg & 16)) deadline((I + 2) >> 2, I, neh);
       stamp(5);
       __builtin_amdgcn_sched_barrier(0);
@@ -614,7 +769,10 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
     }
   }
   if constexpr (GRP == 0) __builtin_amdgcn_s_barrier();    // balance group 1's extra barrier
-  if (!(dbg & 2)) persist_epilogue<T, C, EPI>(p, epi_item(cur), acc, bias_lds, lane, wm, wn);
+  if (!(dbg & 2)) {
+    epilogue_half(0);
+    epilogue_half(1);
+  }
 }
 
 template <typename T, bool AK, bool BK, int EPI, int MODE = 0>
@@ -636,6 +794,21 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p) {
   const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   if ((threadIdx.x >> 6) < 4) pp_run<T, AK, BK, EPI, 0, MODE>(p, lbase, smem, bias_lds, nm, W);
   else pp_run<T, AK, BK, EPI, 1, MODE>(p, lbase, smem, bias_lds, nm, W);
+}
+
+// split-K form (cfg 44): items are (tile, split) — the weight-gradient GEMMs (M, N = features,
+// K = B x T rows: a few 256 x 256 tiles over a long K); fp32 partial slabs (+ the A row sums) for
+// splitk_reduce_kernel, which jmt_gemm launches next
+template <typename T, bool AK, bool BK, int SPL>
+__global__ __launch_bounds__(512) void gemm_pp_split_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int W = p.tiles_m * p.tiles_n * p.batch0 * p.batch1 * p.splits;
+  const int G = gridDim.x;
+  const int nm = (W - (int)blockIdx.x + G - 1) / G;
+  if (nm <= 0 || p.K < 64) return;
+  const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  if ((threadIdx.x >> 6) < 4) pp_run<T, AK, BK, 0, 0, 0, SPL>(p, lbase, smem, nullptr, nm, W);
+  else pp_run<T, AK, BK, 0, 1, 0, SPL>(p, lbase, smem, nullptr, nm, W);
 }
 
 // the persistent configuration (gemm_persist_kernel): cfg 40 = Cfg5's tile (128-B K-tiles, 2
@@ -677,7 +850,7 @@ static void launch_pp_epi(const GemmParams& p, int blocks, hipStream_t st) {
   void (*fn)(GemmParams) = gemm_pp_kernel<T, AK, BK, EPI>;
   if constexpr (EPI == 0 && sizeof(T) == 2) {
     if (p.dbg & 8) fn = gemm_pp_kernel<T, AK, BK, EPI, 2>;
-    else if (p.dbg & 55) fn = gemm_pp_kernel<T, AK, BK, EPI, 1>;
+    else if (p.dbg & 87) fn = gemm_pp_kernel<T, AK, BK, EPI, 1>;
   }
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
@@ -689,13 +862,15 @@ static void launch_pp_epi(const GemmParams& p, int blocks, hipStream_t st) {
 
 template <typename T, bool AK, bool BK, class C>
 static void launch_persist_cfg(const GemmParams& p, int blocks, hipStream_t st, int cfg) {
-  const int epi = (p.beta != 0.f ? 1 : 0) | (p.aux != nullptr ? 2 : 0);
+  int epi = (p.beta != 0.f ? 1 : 0) | (p.aux != nullptr ? 2 : 0);
+  if (epi == 0 && p.relu) epi = 4;
   if (cfg == 43) {
     switch (epi) {
       case 0: launch_pp_epi<T, AK, BK, 0>(p, blocks, st); break;
       case 1: launch_pp_epi<T, AK, BK, 1>(p, blocks, st); break;
       case 2: launch_pp_epi<T, AK, BK, 2>(p, blocks, st); break;
-      default: launch_pp_epi<T, AK, BK, 3>(p, blocks, st); break;
+      case 3: launch_pp_epi<T, AK, BK, 3>(p, blocks, st); break;
+      default: launch_pp_epi<T, AK, BK, 4>(p, blocks, st); break;
     }
     return;
   }
@@ -703,7 +878,8 @@ static void launch_persist_cfg(const GemmParams& p, int blocks, hipStream_t st, 
     case 0: launch_persist_epi<T, AK, BK, C, 0>(p, blocks, st); break;
     case 1: launch_persist_epi<T, AK, BK, C, 1>(p, blocks, st); break;
     case 2: launch_persist_epi<T, AK, BK, C, 2>(p, blocks, st); break;
-    default: launch_persist_epi<T, AK, BK, C, 3>(p, blocks, st); break;
+    case 3: launch_persist_epi<T, AK, BK, C, 3>(p, blocks, st); break;
+    default: launch_persist_epi<T, AK, BK, C, 4>(p, blocks, st); break;
   }
 }
 
@@ -723,7 +899,59 @@ int launch_gemm_persist(const GemmParams& p, int dt, int ak, int bk, int cfg, in
   return 0;
 }
 
-int num_cus_persist() { return num_cus(); }
+template <typename T, bool AK, bool BK>
+static void launch_pp_split_t(const GemmParams& p, bool rs, int blocks, hipStream_t st) {
+  void (*fn)(GemmParams) = rs ? gemm_pp_split_kernel<T, AK, BK, 2> : gemm_pp_split_kernel<T, AK, BK, 1>;
+  (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(512), (size_t)PP_NSLOT * PP_SLOT, st, p);
+}
+
+template <typename T>
+static void launch_pp_split_l(const GemmParams& p, int ak, int bk, bool rs, int blocks,
+                              hipStream_t st) {
+  if (ak && bk) launch_pp_split_t<T, true, true>(p, rs, blocks, st);
+  else if (ak) launch_pp_split_t<T, true, false>(p, rs, blocks, st);
+  else if (bk) launch_pp_split_t<T, false, true>(p, rs, blocks, st);
+  else launch_pp_split_t<T, false, false>(p, rs, blocks, st);
+}
+
+// the split-K ping-pong launch (cfg 44): p.splits, p.tiles_m / tiles_n (256 x 256), p.ws and
+// (row sums) p.dbias_ws set by the caller; the caller launches the slab reduction after it
+void launch_gemm_pp_split(const GemmParams& p, int dt, int ak, int bk, bool rs, int blocks,
+                          hipStream_t st) {
+  if (dt == JMT_BF16) launch_pp_split_l<__bf16>(p, ak, bk, rs, blocks, st);
+  else launch_pp_split_l<_Float16>(p, ak, bk, rs, blocks, st);
+}
+
+// cfg 44 eligibility (also the planner's split choice, pp_split_plan): 16-bit A / B, whole
+// 256 x 256 tiles, whole 64-deep K-tiles, and at least 2 K-tiles per split
+bool pp_split_ok(int dt, int M, int N, int K, int splits) {
+  return dt != JMT_F32 && M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && splits >= 2 &&
+         (K / 64) / splits >= 2;
+}
+
+// the split count for cfg 44 on a launch of few tiles over a long K: enough (tile, split) items
+// for every CU, at least 4 K-tiles each; 0 when the shape has tiles enough without splitting,
+// and below 24 tiles, where each CU's 256 KiB fp32 slab outweighs the faster loop and the
+// 128 x 128 split plan stays ahead (TN 512 x 512 x 19200 b3: 62 vs 57 us, 512 x 2048: 70 vs 63;
+// 1024 x 512 b3 / b6, 1536 x 512 b3, 1024 x 3072: 6-10 % faster; profiles/r05/tn_pp_split_ab.txt)
+int pp_split_plan(int dt, int M, int N, int K, int batch) {
+  if (dt == JMT_F32 || M % 256 || N % 256 || K % 64) return 0;
+  const long tiles = (long)(M / 256) * (N / 256) * batch;
+  const int ncu = num_cus_persist();
+  if (tiles * 2 > ncu || tiles < 24) return 0;
+  long s = ncu / tiles;
+  const long smax = (K / 64) / 4;
+  if (s > smax) s = smax;
+  return s >= 2 ? (int)s : 0;
+}
+
+// persistent grid: a multiple of 8 blocks (pitem / pwalk deal items per XCD slot w % 8)
+int num_cus_persist() {
+  const int n = num_cus() & ~7;
+  return n > 0 ? n : 8;
+}
 
 }  // namespace jmt
 

@@ -584,5 +584,11 @@ int num_cus_persist();
 int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int forced);
 // gemm_persist_kernel's limit on the per-column bias staged in LDS (floats, all tables)
 constexpr int kPersistBias = 8192;
+// gemm_persist.hip, split-K ping-pong (cfg 44): the launch (fp32 slabs + optional A row sums;
+// the caller reduces), its preconditions, and the planner's split count for it (0: not used)
+void launch_gemm_pp_split(const GemmParams& p, int dt, int ak, int bk, bool rs, int blocks,
+                          hipStream_t st);
+bool pp_split_ok(int dt, int M, int N, int K, int splits);
+int pp_split_plan(int dt, int M, int N, int K, int batch);
 
 }  // namespace jmt

@@ -1,5 +1,7 @@
 """GEMM micro-benchmark on the JMT step's shapes (bf16), with optional ablations:
-    python scripts/bench_gemm.py [--dbg 0|1|2|3] [--reps 50]
+    python scripts/bench_gemm.py [--dbg 0|1|2|3] [--reps 50] [--cfg 0 43 44] [--only a,b]
+(JMT_GEMM_PPSPLIT=0 in the environment: the weight-gradient shapes take the one-block split-K
+plan instead of the split-K ping-pong kernel, cfg 44)
 Prints per shape: µs/launch, TFLOP/s, and the algorithmic-bytes GB/s."""
 import argparse
 import json
@@ -29,6 +31,11 @@ SHAPES = [
     ("dgrad out1 19200x3072x1024 NN", 19200, 3072, 1024, True, False, 1, BF16, 1),
     ("wgrad out1 1024x3072x19200 TN", 1024, 3072, 19200, False, False, 1, F32, None),
     ("wgrad 512x512x19200 TN", 512, 512, 19200, False, False, 1, F32, None),
+    ("wgrad b3 512x512x19200 TN", 512, 512, 19200, False, False, 3, F32, None),
+    ("wgrad b3 1024x512x19200 TN", 1024, 512, 19200, False, False, 3, F32, None),
+    ("wgrad b6 1024x512x19200 TN", 1024, 512, 19200, False, False, 6, F32, None),
+    ("wgrad b3 1536x512x19200 TN", 1536, 512, 19200, False, False, 3, F32, None),
+    ("wgrad 512x2048x19200 TN", 512, 2048, 19200, False, False, 1, F32, None),
     ("attn S 300x300x512 b64 NT", 300, 300, 512, True, True, 64, F32, 1),
     ("attn PV 300x512x300 b64 NN", 300, 512, 300, True, False, 64, BF16, 1),
     ("attn dK 300x512x300 b64 TN", 300, 512, 300, False, False, 64, BF16, 1),

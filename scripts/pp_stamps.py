@@ -3,8 +3,10 @@ of a step shape with s_memtime stamps of block 0's waves, printed as per-segment
 (median over the K-tiles 2..23, then the first K-tiles raw).
 
     python scripts/pp_stamps.py [--shape NT_b6_1024] [--dbg-extra 0]
-Stamps per (wave, K-tile, phase): 0 load-segment start, 1 LDS reads issued, 2 DMA issued,
-3 deadline wait done, 4 after the barrier (MFMA segment start), 5 MFMAs issued (+ deadline)."""
+Stamps per (wave, K-tile, phase): 0 load-segment start, 6 epilogue half done, 7 stream K-tile
+step done, 1 LDS reads issued, 2 DMA issued, 3 deadline wait done, 4 after the barrier (MFMA
+segment start), 5 MFMAs issued (+ deadline).  Per-K-tile rows list, per phase: [epilogue, step,
+reads, dma, deadline, barrier1, mfma, barrier2]."""
 import argparse
 import ctypes as C
 import json
@@ -46,13 +48,13 @@ def main():
             ops.gemm(**kw)
         torch.cuda.synchronize()
     lib.jmt_gemm_set_debug(0)
-    n = 8 * PP_STK * 4 * 6
+    n = 8 * PP_STK * 4 * 8
     buf = (C.c_uint64 * n)()
     fn = lib.jmt_gemm_pp_stamps_read
     fn.restype = C.c_int
     fn.argtypes = [C.c_void_p, C.c_int]
     assert fn(buf, n) == n
-    st = [[[[buf[((w * PP_STK + t) * 4 + p) * 6 + e] for e in range(6)] for p in range(4)]
+    st = [[[[buf[((w * PP_STK + t) * 4 + p) * 8 + e] for e in range(8)] for p in range(4)]
            for t in range(PP_STK)] for w in range(8)]
     names = ["reads", "dma", "deadline", "barrier1", "mfma", "barrier2"]
     for w in (0, 4):
@@ -67,6 +69,14 @@ def main():
                     if v is not None and 0 <= v < 10 ** 7:
                         seg[k].append(v)
         kt = [st[w][t + 1][0][0] - st[w][t][0][0] for t in range(2, PP_STK - 1)]
+        for t in range(4, 11):
+            row = []
+            for p in range(4):
+                s = st[w][t][p]
+                nxt = st[w][t][p + 1][0] if p < 3 else st[w][t + 1][0][0]
+                row.append([s[6] - s[0], s[7] - s[6], s[1] - s[7], s[2] - s[1], s[3] - s[2],
+                            s[4] - s[3], s[5] - s[4], nxt - s[5]])
+            print(json.dumps({"wave": w, "ktile": t, "segs": row}))
         print(json.dumps({"shape": args.shape, "wave": w,
                           "median_cycles": {k: statistics.median(v) for k, v in seg.items() if v},
                           "ktile_cycles_median": statistics.median(kt),

@@ -124,3 +124,21 @@ def test_host_code_under_asan():
 
 def test_default_build_has_no_bounds_counters():
     assert _lib.load().jmt_bounds_violations(0) == -1
+
+
+def test_planner_split_k_ping_pong_choice():
+    """The planner's split count for the weight-gradient shapes (a few 256 x 256 tiles over
+    B x T rows) comes from the split-K ping-pong kernel (cfg 44): one (tile, split) item per CU
+    (256 here: the CU count falls back to 256 without a device), at least 4 K-tiles per split;
+    shapes with tiles enough, under 24 tiles, or not whole 256 x 256 tiles keep the previous
+    plan."""
+    from jmt._lib import BF16
+    lib = _lib.load()
+    plan = lambda M, N, K, b: lib.jmt_gemm_plan_splits(BF16, M, N, K, b)
+    assert plan(1024, 512, 19200, 6) == 5          # 48 tiles
+    assert plan(1024, 512, 19200, 3) == 10         # 24 tiles
+    assert plan(3072, 1024, 1536, 1) == 5          # 48 tiles
+    assert plan(19200, 512, 512, 3) == 1           # 450 tiles: no split
+    # under 24 tiles (and M not a multiple of 256) the 128 x 128 split plan keeps its choice
+    assert plan(512, 512, 19200, 3) != 21
+    assert plan(128, 1024, 19200, 2) != 256 // 8

@@ -1076,6 +1076,54 @@ def test_layernorm_grouped_equals_per_group(dsum, cd):
             assert close(a[3][i], b[3][i])
 
 
+@pytest.mark.parametrize("ak,bk", [(False, False), (True, True), (True, False)])
+def test_gemm_pp_split_k(ak, bk):
+    """Split-K ping-pong kernel (cfg 44, gemm_persist.hip gemm_pp_split_kernel): items are
+    (256 x 256 tile, split) with balanced K-tile ranges, fp32 partial slabs reduced by
+    splitk_reduce_kernel.  vs torch fp32 with beta = 1 accumulation into C, for the planner's own
+    split count (the weight-gradient shapes) and forced uneven splits; the A row sums (dbias,
+    TN layout only) within fp32 accumulation noise and C bit-identical with and without them."""
+    from jmt import _lib
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(44)
+    bf = torch.bfloat16
+    cases = [(1024, 512, 19200, 3, None), (1024, 1536, 4096, 1, None), (512, 256, 1344, 2, 7)]
+    for (M, N, K, nb, splits) in cases:
+        if splits is None:
+            assert ops.auto_splits(M, N, K, nb, BF16) >= 2
+        A, Al, lda, sa = _operand(M, K, ak, BF16, batch=nb, gen=g)
+        Bs, Bl_t, ldb, sb = _operand(N, K, bk, BF16, batch=nb, gen=g)
+        Bl = Bl_t.transpose(1, 2)
+        C0 = torch.randn(nb, M, N, device=DEV, generator=g)
+        outs = []
+        for cfg in (44, 5):                 # 5: the one-block-per-tile split-K kernel
+            for rs in ((False, True) if (not ak and not bk and cfg == 44) else (False,)):
+                C = C0.clone()
+                db = [torch.zeros(M, device=DEV) for _ in range(nb)] if rs else None
+                lib.jmt_gemm_set_debug(cfg << 8)
+                try:
+                    ops.gemm(M=M, N=N, K=K, ab_dtype=BF16, c_dtype=F32,
+                             a=[A[i].data_ptr() for i in range(nb)], lda=lda, a_kmajor=ak,
+                             a_mode=1, b=[Bs[i].data_ptr() for i in range(nb)], ldb=ldb,
+                             b_kmajor=bk, b_mode=1, c=[C[i].data_ptr() for i in range(nb)],
+                             ldc=N, c_mode=1, batch0=nb, beta=1.0, splits=splits,
+                             dbias_tab=db, device=DEV)
+                finally:
+                    lib.jmt_gemm_set_debug(0)
+                torch.cuda.synchronize()
+                outs.append(C)
+                for i in range(nb):
+                    ref = C0[i] + Al[i] @ Bl[i]
+                    err = (C[i] - ref).abs().max().item()
+                    assert err <= 2e-3 * (Al[i].abs() @ Bl[i].abs()).max().item(), (M, N, K, cfg, err)
+                    if rs:
+                        rref = Al[i].sum(1)
+                        rerr = (db[i] - rref).abs().max().item()
+                        assert rerr <= 1e-6 * Al[i].abs().sum(1).max().item() + 1e-5, (M, K, rerr)
+        if not ak and not bk:
+            assert torch.equal(outs[0], outs[1]), "row sums changed C"
+
+
 @pytest.mark.parametrize("cfg", [0, 1, 5, 10, 11, 20, 21])
 @pytest.mark.parametrize("dt", [BF16, F16])
 def test_gemm_wgrad_row_sums_bias_grad(cfg, dt):
