@@ -799,6 +799,11 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p) {
 // split-K form (cfg 44): items are (tile, split) — the weight-gradient GEMMs (M, N = features,
 // K = B x T rows: a few 256 x 256 tiles over a long K); fp32 partial slabs (+ the A row sums) for
 // splitk_reduce_kernel, which jmt_gemm launches next
+// (An in-launch reduction — the S blocks of a tile meeting at a per-tile counter, then each
+// reducing its 256 / S rows over all S slabs — measured slower than the separate
+// splitk_reduce_kernel launch on every weight-gradient shape, 5-10 %: the reduce loop of one
+// 8-wave block per CU keeps too few slab loads in flight; profiles/r05/tn_fused_reduce_ab.txt.)
+
 template <typename T, bool AK, bool BK, int SPL>
 __global__ __launch_bounds__(512) void gemm_pp_split_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -901,7 +906,8 @@ int launch_gemm_persist(const GemmParams& p, int dt, int ak, int bk, int cfg, in
 
 template <typename T, bool AK, bool BK>
 static void launch_pp_split_t(const GemmParams& p, bool rs, int blocks, hipStream_t st) {
-  void (*fn)(GemmParams) = rs ? gemm_pp_split_kernel<T, AK, BK, 2> : gemm_pp_split_kernel<T, AK, BK, 1>;
+  void (*fn)(GemmParams) =
+      rs ? gemm_pp_split_kernel<T, AK, BK, 2> : gemm_pp_split_kernel<T, AK, BK, 1>;
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(512), (size_t)PP_NSLOT * PP_SLOT, st, p);
@@ -940,7 +946,12 @@ int pp_split_plan(int dt, int M, int N, int K, int batch) {
   if (dt == JMT_F32 || M % 256 || N % 256 || K % 64) return 0;
   const long tiles = (long)(M / 256) * (N / 256) * batch;
   const int ncu = num_cus_persist();
-  if (tiles * 2 > ncu || tiles < 24) return 0;
+  static int min_tiles = -1;                  // development: JMT_GEMM_PPSPLIT_MIN_TILES
+  if (min_tiles < 0) {
+    const char* e = getenv("JMT_GEMM_PPSPLIT_MIN_TILES");
+    min_tiles = e ? atoi(e) : 24;
+  }
+  if (tiles * 2 > ncu || tiles < min_tiles) return 0;
   long s = ncu / tiles;
   const long smax = (K / 64) / 4;
   if (s > smax) s = smax;
@@ -984,12 +995,13 @@ int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int 
   if (forced == 40 || forced == 43) return forced;
   if (forced != 0 || env == 0) return 0;
   if (env == 40 || env == 43) return env;
-  // default: the 128-B-K-tile form wherever the launch has at least 1.5 tiles per CU (below
-  // that the 160x256 / split tiles of the one-block-per-tile kernel quantise better: NT
-  // 19200x512x2048 53 vs 68 us); it beat the one-block-per-tile kernel on every batched step
-  // shape by 9-20 % and cfg 41 everywhere (profiles/r04/gemm_persist_vs_vendor_a.jsonl)
+  // default: the ping-pong kernel (cfg 43) wherever the launch has at least 1.5 tiles per CU
+  // (below that the 160x256 / split tiles of the one-block-per-tile kernel quantise better: NT
+  // 19200x512x2048 53 vs 68 us).  cfg 40 beat the one-block-per-tile kernel on every batched
+  // step shape by 9-20 % (profiles/r04/gemm_persist_vs_vendor_a.jsonl); cfg 43 beats cfg 40 by
+  // 14-25 % on the same shapes (profiles/r05/gemm_pp_vs_persist.txt)
   const long W = (long)(d->M / 256) * (d->N / 256) * batch0 * (d->batch1 < 1 ? 1 : d->batch1);
-  return W * 2 >= 3L * num_cus() ? 40 : 0;
+  return W * 2 >= 3L * num_cus() ? 43 : 0;
 }
 
 }  // namespace jmt

@@ -573,6 +573,100 @@ __device__ __forceinline__ void load4_guard(const O* row, int n, int lim, bool v
   }
 }
 
+// The reduce + epilogue of W (1 or 4) consecutive outputs (b, m, n..n+W-1): the splits' fp32
+// partial slabs summed in split order (the same order, so the same bits, wherever it runs),
+// then alpha, bias, beta * C, ReLU, the ReLU mask; the A row sums' split partials folded by the
+// thread of column 0.
+template <typename O, int W>
+__device__ __forceinline__ void reduce_outputs(const GemmParams& p, int b, int m, int n) {
+  const int nb = p.batch0 * p.batch1;
+  const int64_t per = (int64_t)p.M * p.N;
+  const int64_t mn = (int64_t)m * p.N + n;
+  float v[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) v[i] = 0.f;
+  const int64_t sstride = (int64_t)nb * per;
+  const float* src0 = p.ws + (int64_t)b * per + mn;
+  int s = 0;
+  if constexpr (W == 4) {
+    // eight (then four) slab loads in flight per step, summed in split order (the same sums as
+    // four at a time: bit-identical; no measurable change in the step, profiles/r04/
+    // splitk_reduce_depth_ab.txt)
+    for (; s + 8 <= p.splits; s += 8) {
+      float4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = *(const float4*)(src0 + (s + u) * sstride);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[0] += t[u].x; v[1] += t[u].y; v[2] += t[u].z; v[3] += t[u].w;
+      }
+    }
+    for (; s + 4 <= p.splits; s += 4) {
+      float4 t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = *(const float4*)(src0 + (s + u) * sstride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[0] += t[u].x; v[1] += t[u].y; v[2] += t[u].z; v[3] += t[u].w;
+      }
+    }
+  }
+  for (; s < p.splits; ++s) {
+    const float* src = src0 + s * sstride;
+    if constexpr (W == 4) {
+      const float4 t = *(const float4*)src;
+      v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
+    } else {
+      v[0] += *src;
+    }
+  }
+  const int b0 = b / p.batch1, b1 = b % p.batch1;
+  if (p.n_dbias > 0 && n == 0 && p.dbias_tab[b0]) {   // the A row sums' split partials
+    const float* src = p.dbias_ws + (int64_t)b * p.M + m;
+    float r = 0.f;
+    for (int t = 0; t < p.splits; ++t) r += src[(int64_t)t * nb * p.M];
+    float* d = p.dbias_tab[b0];
+    d[m] = (p.dbias_acc ? d[m] : 0.f) + r;
+  }
+  const float* biasp = p.n_bias > 0 ? p.bias_tab[b0] : p.bias;
+  O* cp;
+  int64_t cbase;
+  if (p.c_mode == 1) {
+    cp = (O*)p.c_ptr[b0];
+    cbase = (int64_t)b1 * p.sC1;
+  } else {
+    cp = (O*)p.c_ptr[0];
+    cbase = (int64_t)b0 * p.sC0 + (int64_t)b1 * p.sC1;
+  }
+  const int64_t co = cbase + (int64_t)m * p.ldc + n;
+  const O* auxp = (const O*)p.aux;
+  float cin[W], ain[W];
+  if constexpr (W == 4) {
+    if (p.beta != 0.f) load4_guard(cp + co, 0, 4, true, cin);
+    if (auxp) load4_guard(auxp + cbase + (int64_t)m * p.ldaux + n, 0, 4, true, ain);
+  } else {
+    if (p.beta != 0.f) cin[0] = to_f(cp[co]);
+    if (auxp) ain[0] = to_f(auxp[cbase + (int64_t)m * p.ldaux + n]);
+  }
+  O out[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    float x = v[i] * p.alpha;
+    if (p.bias_mode == 1) x += biasp[n + i];
+    else if (p.bias_mode == 2) x += biasp[m];
+    if (p.beta != 0.f) x += p.beta * cin[i];
+    if (p.relu) x = fmaxf(x, 0.f);
+    if (auxp && !(ain[i] > 0.f)) x = 0.f;
+    out[i] = from_f<O>(x);
+  }
+  if constexpr (W == 4) {
+    if constexpr (sizeof(O) == 4) *(float4*)(cp + co) = *(const float4*)out;
+    else *(uint2*)(cp + co) = *(const uint2*)out;
+  } else {
+    cp[co] = out[0];
+  }
+}
+
 // gemm_persist.hip: launch the persistent kernel (cfg 40) on `blocks` blocks
 int launch_gemm_persist(const GemmParams& p, int dt, int ak, int bk, int cfg, int blocks,
                         hipStream_t st);
