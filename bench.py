@@ -36,7 +36,7 @@ for _p in (REPO, PKG):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-PROFILE_TAG = "r04"            # profiles/<tag>_pmc_bench/ (PMC traffic), <tag>_family_trace.json
+PROFILE_TAG = "r05"            # profiles/<tag>_pmc_bench/ (PMC traffic), <tag>_family_trace.json
 PEAK_BF16_TFLOPS = 2516.6      # 256 CU x 4 SIMD x 1024 flop/clk (16x16x32 bf16 / 16 cyc) x 2.4 GHz
 PEAK_HBM_GBS = 8000.0
 D_A, D_V, E = 1024, 2048, 512
