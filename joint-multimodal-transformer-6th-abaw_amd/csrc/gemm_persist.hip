@@ -608,9 +608,17 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
   // intervals in (i_last, i_now] (2 each, while pieces exist) and an epilogue of this K-tile.
   // neh: epilogue halves (EPH operations each) issued after the wave's last piece of g (the
   // caller knows them from the schedule: 0, 1 or 2)
-  auto deadline = [&](int g, int i_now, int neh) {
+  // steady: the caller's K-tile t has t + 3 <= nT, so i_now <= 8 t + 7 <= npieces - 1 - PP_D
+  // and g < 2 nT (one flag per K-tile instead of two compares per deadline)
+  auto deadline = [&](int g, int i_now, int neh, bool steady) {
+    if (steady) {                                          // constant counts
+      if (neh == 0) wait_vmcnt<NSTEADY>();
+      else if (neh == 1) wait_vmcnt<NSTEADY_EP1>();
+      else wait_vmcnt<NSTEADY_EP2>();
+      return;
+    }
     if (g >= 2 * nT) return;
-    if (i_now <= npieces - 1 - PP_D) {                     // steady state: constant counts
+    if (i_now <= npieces - 1 - PP_D) {
       if (neh == 0) wait_vmcnt<NSTEADY>();
       else if (neh == 1) wait_vmcnt<NSTEADY_EP1>();
       else wait_vmcnt<NSTEADY_EP2>();
@@ -629,7 +637,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
     if (P >= 8 && P - 2 < 8) next_ktile();                 // (PP_D <= 16: K-tiles 0 and 1)
     if (P < npieces) issue(P >> 2, P & 3);
   }
-  deadline(0, -1, 0);
+  deadline(0, -1, 0, false);
   __builtin_amdgcn_s_barrier();
   if constexpr (GRP == 1) __builtin_amdgcn_s_barrier();    // group 1 runs one barrier behind
   __builtin_amdgcn_sched_barrier(0);
@@ -639,7 +647,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
   for (int i = 0; i < C::TM; ++i)
 #pragma unroll
     for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  F fa[4], fb[4];
+  F fa[4] = {}, fb[4] = {};
   PWalk cur_w = pwalk_init(p, blockIdx.x, W, G);
   PItem cur = pwalk_item(p, cur_w);
   int cur_left = cur.len;
@@ -666,6 +674,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
 
   const bool stamping = STAMP && blockIdx.x == 0 && lane == 0;
   for (int t = 0; t < nT; ++t) {
+    const bool steady = t + 3 <= nT;
 #pragma unroll
     for (int pp = 0; pp < 4; ++pp) {
       const int ks = pp >> 1, qm = pp & 1;
@@ -705,14 +714,16 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
         next_ktile();
       stamp(7);
       const char* slot = smem + ((2 * t + ks) & (PP_NSLOT - 1)) * PP_SLOT;
-      if (qm == 0) {
+      if (!(dbg & 128)) {                                  // (ablation 128: no fragment reads)
+        if (qm == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          fb[j] = read_frag16<T, BK, 64, 256>(slot + 16384, wn * C::WTN + 16 * j, 0);
+          for (int j = 0; j < 4; ++j)
+            fb[j] = read_frag16<T, BK, 64, 256>(slot + 16384, wn * C::WTN + 16 * j, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          fa[i] = read_frag16<T, AK, 64, 256>(slot, wm * C::WTM + 64 * qm + 16 * i, 0);
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        fa[i] = read_frag16<T, AK, 64, 256>(slot, wm * C::WTM + 64 * qm + 16 * i, 0);
       stamp(1);
       if (!(dbg & 4) && I + PP_D < npieces) issue(2 * (t + (L >> 3)) + ((L >> 2) & 1), L & 3);
       stamp(2);
@@ -723,7 +734,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
       // piece of k-half 2t + 2 went out after it, in the same phase-0 segment)
       const int neh = pp == 1 ? (epB ? 2 : 0)
                               : (GRP == 1 && epB ? 1 : 0) + (epA ? 1 : 0);
-      if (GRP == 1 && (pp & 1) && !(dbg & 16)) deadline((I + 1) >> 2, I, neh);
+      if (GRP == 1 && (pp & 1) && !(dbg & 16)) deadline((I + 1) >> 2, I, neh, steady);
       stamp(3);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -761,7 +772,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
 #pragma unroll
           for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if (GRP == 0 && (pp & 1) && !(dbg & 16)) deadline((I + 2) >> 2, I, neh);
+      if (GRP == 0 && (pp & 1) && !(dbg & 16)) deadline((I + 2) >> 2, I, neh, steady);
       stamp(5);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -855,7 +866,7 @@ static void launch_pp_epi(const GemmParams& p, int blocks, hipStream_t st) {
   void (*fn)(GemmParams) = gemm_pp_kernel<T, AK, BK, EPI>;
   if constexpr (EPI == 0 && sizeof(T) == 2) {
     if (p.dbg & 8) fn = gemm_pp_kernel<T, AK, BK, EPI, 2>;
-    else if (p.dbg & 87) fn = gemm_pp_kernel<T, AK, BK, EPI, 1>;
+    else if (p.dbg & 215) fn = gemm_pp_kernel<T, AK, BK, EPI, 1>;
   }
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
