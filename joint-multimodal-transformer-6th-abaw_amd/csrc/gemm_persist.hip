@@ -954,7 +954,9 @@ bool pp_split_ok(int dt, int M, int N, int K, int splits) {
 // 128 x 128 split plan stays ahead (TN 512 x 512 x 19200 b3: 62 vs 57 us, 512 x 2048: 70 vs 63;
 // 1024 x 512 b3 / b6, 1536 x 512 b3, 1024 x 3072: 6-10 % faster; profiles/r05/tn_pp_split_ab.txt)
 int pp_split_plan(int dt, int M, int N, int K, int batch) {
-  if (dt == JMT_F32 || M % 256 || N % 256 || K % 64) return 0;
+  // long K only: at realdata's K = 1024 rows a split is a few K-tiles, its pipeline prologue and
+  // slab epilogue dominate (realdata 1.00 -> 1.22 ms/step; profiles/r05/cfg_gemm_ab.txt)
+  if (dt == JMT_F32 || M % 256 || N % 256 || K % 64 || K < 8192) return 0;
   const long tiles = (long)(M / 256) * (N / 256) * batch;
   const int ncu = num_cus_persist();
   static int min_tiles = -1;                  // development: JMT_GEMM_PPSPLIT_MIN_TILES

@@ -130,14 +130,15 @@ def test_planner_split_k_ping_pong_choice():
     """The planner's split count for the weight-gradient shapes (a few 256 x 256 tiles over
     B x T rows) comes from the split-K ping-pong kernel (cfg 44): one (tile, split) item per CU
     (256 here: the CU count falls back to 256 without a device), at least 4 K-tiles per split;
-    shapes with tiles enough, under 24 tiles, or not whole 256 x 256 tiles keep the previous
-    plan."""
+    shapes with tiles enough, under 24 tiles, K under 8192 rows or not whole 256 x 256 tiles keep
+    the previous plan."""
     from jmt._lib import BF16
     lib = _lib.load()
     plan = lambda M, N, K, b: lib.jmt_gemm_plan_splits(BF16, M, N, K, b)
     assert plan(1024, 512, 19200, 6) == 5          # 48 tiles
     assert plan(1024, 512, 19200, 3) == 10         # 24 tiles
-    assert plan(3072, 1024, 1536, 1) == 5          # 48 tiles
+    assert plan(1024, 3072, 19200, 1) == 5         # 48 tiles (out_layer1's weight gradient)
+    assert plan(3072, 1024, 1536, 1) == 1          # short K (< 8192 rows): no cfg 44
     assert plan(19200, 512, 512, 3) == 1           # 450 tiles: no split
     # under 24 tiles (and M not a multiple of 256) the 128 x 128 split plan keeps its choice
     assert plan(512, 512, 19200, 3) != 21
