@@ -821,7 +821,7 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
                         (cfg == 44 || (cfg == 0 && pp_split_env() &&
                                        pp_split_plan(dt, d->M, d->N, d->K, batch0 * batch1)));
   if (cfg == 44) cfg = 0;
-  if (cfg == 40 || cfg == 43) cfg = 5;      // persistent configs not applicable: same tile
+  if (cfg == 40 || cfg == 43 || cfg == 45) cfg = 5;   // persistent configs not applicable
   if (dt == JMT_F32 && cfg >= 10) cfg = 1;   // occupancy / 160-row configs: 16-bit only
   if (cfg == 32 && !d->a_kmajor) cfg = 5;    // 160-row tile: K-major A only
   if (!cfg) {

@@ -807,6 +807,223 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p) {
   else pp_run<T, AK, BK, EPI, 1, MODE>(p, lbase, smem, bias_lds, nm, W);
 }
 
+// ---------------------------------------------------------------- ping-pong, 32-MFMA phases
+// cfg 45 (the default where the persistent path applies): the ping-pong schedule above with ONE
+// phase per k-half — the whole 32-deep k-half over all 8 row sub-tiles of the wave, 12 fragment
+// reads and 32 MFMAs — so a K-tile is 2 phases = 4 barrier intervals instead
+// of 8 (the measured ≈ 250 cycles of barrier and bookkeeping per interval, halved per FLOP).
+// DMA: interval I issues pieces 2 I + P2_D, 2 I + P2_D + 1 (P2_D = 10, the most the 4-slot ring
+// allows: k-half g + 4 reuses g's slot, whose last reads retire in interval 2 g + 2); with P2_D
+// even, group 0 (even intervals) always issues the B halves of k-half m + 2 at its phase m, group
+// 1 the A halves of k-half m + 3.  Deadline of k-half g, before barrier 2 g - 1: group 0 in its
+// MFMA segment of phase g - 1 (younger: its phase g - 1 pieces, 4 ops, and that load segment's
+// epilogue), group 1 in its load segment of phase g - 1 after its pieces (younger: phases g - 2
+// and g - 1, 8 ops, and their epilogues).  The epilogue of an item is whole, in each group's load
+// segment of the next item's first phase (every phase writes all 8 row sub-tiles).
+constexpr int P2_D = 10;
+static_assert(P2_D % 2 == 0 && P2_D <= 10, "pp2 deadline counts are derived for an even P2_D <= 10");
+
+template <typename T, bool AK, bool BK, int EPI, int GRP>
+__device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, const char* smem,
+                                        const float* bias_lds, int nm, int W) {
+  using C = CfgPP;
+  typedef typename Frag16<T>::t F;
+  constexpr bool ISA = GRP == 1;                           // this group's operand: A (else B)
+  constexpr bool KM = ISA ? AK : BK;
+  constexpr int NST = C::TM * (C::TN / 2);
+  constexpr int NLD = ((EPI & 1) ? C::TM * C::TN : 0) + ((EPI & 2) ? C::TM * C::TN : 0);
+  constexpr int EPO = NST + NLD;                           // VMEM operations of one epilogue
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wl = wid & 3;
+  constexpr int wm = GRP;
+  const int wn = wl;
+  const int G = gridDim.x;
+  const int nkt = p.K >> 6;
+  const int nT = nm * nkt;
+  const int nh = 2 * nT;                                   // k-halves of the block's stream
+  const int64_t ld = ISA ? p.lda : p.ldb;
+  // per-lane byte offsets of this wave's instructions 2 wl, 2 wl + 1 of each half (h) of its
+  // operand's k-half image, relative to the operand's K-tile base
+  int64_t off[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      int row, kk;
+      chunk_src<T, KM, 64, 256>((8 * h + 2 * wl + e) * 64 + lane, row, kk);
+      off[h][e] = (KM ? (int64_t)row * ld + kk : (int64_t)kk * ld + row) * (int64_t)sizeof(T);
+    }
+  const int64_t dk = (KM ? (int64_t)64 : (int64_t)64 * ld) * (int64_t)sizeof(T);   // K-tile
+  const int64_t hk = dk / 2;                                                          // k-half
+  const int seg = (ISA ? p.a_mode : p.b_mode) == 2 ? (ISA ? p.a_kseg : p.b_kseg) / 64 : 1 << 30;
+
+  PWalk iss_w = pwalk_init(p, blockIdx.x, W, G);
+  PItem iss_it = pwalk_item(p, iss_w);
+  int iss_k = 0, iss_kt = 0, left = 0;
+  const char* ps[2][2];
+  auto set_stream = [&]() {
+    const int k0 = iss_kt * 64;
+    int kl;
+    const T* X = ISA ? operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, iss_it.b0, iss_it.b1,
+                                       p.a_kseg, k0, kl)
+                     : operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, iss_it.b0, iss_it.b1,
+                                       p.b_kseg, k0, kl);
+    const int r0 = ISA ? iss_it.m0 : iss_it.n0;
+    const char* sx = (const char*)(KM ? X + (int64_t)r0 * ld + kl : X + (int64_t)kl * ld + r0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) ps[h][e] = sx + off[h][e];
+    left = seg - (kl >> 6);
+  };
+  auto next_ktile = [&]() {
+    if (++iss_kt == nkt) {
+      iss_kt = 0;
+      if (++iss_k < nm) {
+        pwalk_next(p, iss_w);
+        iss_it = pwalk_item(p, iss_w);
+        set_stream();
+      }
+    } else if (--left == 0) {
+      set_stream();
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) ps[h][e] += dk;
+    }
+  };
+  // this wave's 4 instructions of k-half g (its operand's two halves) from the current K-tile
+  auto issue = [&](int g) {
+    const uint32_t dst = lbase + (g & 3) * PP_SLOT + (ISA ? 0 : 16384) + 2 * wl * 1024;
+    const int64_t kh = (g & 1) ? hk : 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) glds16_at(ps[h][e] + kh, dst + (8 * h + e) * 1024);
+  };
+  auto first = [&](int m) { return m > 0 && m < nh && m % (2 * nkt) == 0; };
+  // k-half g retired by this wave (at phase g - 1); counts as in the header comment, rounded
+  // down near the stream's end
+  auto deadline = [&](int g) {
+    if (g >= nh) return;
+    const int m = g - 1;
+    if constexpr (GRP == 0) {
+      // younger: its piece of k-half m + 2 (phase m) and phase m's epilogue
+      const int n = (m + 2 < nh ? 4 : 0) + (first(m) ? EPO : 0);
+      if (n == 4) wait_vmcnt<4>();
+      else wait_vm_le(n);
+    } else {
+      // younger: its pieces of k-halves m + 2 (phase m - 1) and m + 3 (phase m)
+      const int n = (m + 2 < nh ? 4 : 0) + (m + 3 < nh ? 4 : 0) +
+                    ((first(m - 1) ? 1 : 0) + (first(m) ? 1 : 0)) * EPO;
+      if (n == 8) wait_vmcnt<8>();
+      else wait_vm_le(n);
+    }
+  };
+
+  // prologue: group 0 the B halves of k-halves 0, 1; group 1 the A halves of 0, 1, 2
+  set_stream();
+  if constexpr (GRP == 0) {
+    issue(0);
+    issue(1);
+    wait_vmcnt<4>();                                       // k-half 0 retired
+  } else {
+    issue(0);
+    if (nh > 1) issue(1);
+    if (nh > 2) {
+      next_ktile();
+      issue(2);
+    }
+    wait_vm_le((nh > 1 ? 4 : 0) + (nh > 2 ? 4 : 0));
+  }
+  __builtin_amdgcn_s_barrier();
+  if constexpr (GRP == 1) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  f32x4 acc[C::TM][C::TN];
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  F fa[8] = {}, fb[4] = {};
+  PWalk cur_w = pwalk_init(p, blockIdx.x, W, G);
+  PItem cur = pwalk_item(p, cur_w);
+  int cur_left = nkt;
+  for (int t = 0; t < nT; ++t) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int m = 2 * t + ks;
+      // ---- load segment
+      if (ks == 0) {
+        if (cur_left == 0) {                               // previous item done: its epilogue
+          persist_epilogue<T, C, EPI>(p, cur, acc, bias_lds, lane, wm, wn);
+#pragma unroll
+          for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          pwalk_next(p, cur_w);
+          cur = pwalk_item(p, cur_w);
+          cur_left = nkt;
+        }
+        --cur_left;
+      }
+      // stream step: group 0 issues k-half m + 2 (K-tile t + 1), group 1 k-half m + 3
+      if ((GRP == 0 && ks == 0) || (GRP == 1 && ks == 1)) next_ktile();
+      const char* slot = smem + (m & 3) * PP_SLOT;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fb[j] = read_frag16<T, BK, 64, 256>(slot + 16384, wn * C::WTN + 16 * j, 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        fa[i] = read_frag16<T, AK, 64, 256>(slot, wm * C::WTM + 16 * i, 0);
+      {
+        const int g = m + (GRP == 0 ? 2 : 3);
+        if (g < nh) issue(g);
+      }
+      if constexpr (GRP == 1) deadline(m + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- MFMA segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr (GRP == 0) deadline(m + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if constexpr (GRP == 0) __builtin_amdgcn_s_barrier();
+  persist_epilogue<T, C, EPI>(p, cur, acc, bias_lds, lane, wm, wn);
+}
+
+template <typename T, bool AK, bool BK, int EPI>
+__global__ __launch_bounds__(512) void gemm_pp2_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* bias_lds = (float*)(smem + PP_NSLOT * PP_SLOT);
+  const int W = p.tiles_m * p.tiles_n * p.batch0 * p.batch1;
+  const int G = gridDim.x;
+  const int nm = (W - (int)blockIdx.x + G - 1) / G;
+  if (p.bias_mode == 1) {
+    const int nb = (p.n_bias > 0 ? p.batch0 : 1) * p.N;
+    for (int i = threadIdx.x; i < nb; i += 512) {
+      const int b = i / p.N;
+      bias_lds[i] = (p.n_bias > 0 ? p.bias_tab[b] : p.bias)[i - b * p.N];
+    }
+  }
+  __syncthreads();
+  if (nm <= 0 || p.K < 64) return;
+  const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  if ((threadIdx.x >> 6) < 4) pp2_run<T, AK, BK, EPI, 0>(p, lbase, smem, bias_lds, nm, W);
+  else pp2_run<T, AK, BK, EPI, 1>(p, lbase, smem, bias_lds, nm, W);
+}
+
 // split-K form (cfg 44): items are (tile, split) — the weight-gradient GEMMs (M, N = features,
 // K = B x T rows: a few 256 x 256 tiles over a long K); fp32 partial slabs (+ the A row sums) for
 // splitk_reduce_kernel, which jmt_gemm launches next
@@ -876,10 +1093,31 @@ static void launch_pp_epi(const GemmParams& p, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(512), lds, st, p);
 }
 
+template <typename T, bool AK, bool BK, int EPI>
+static void launch_pp2_epi(const GemmParams& p, int blocks, hipStream_t st) {
+  void (*fn)(GemmParams) = gemm_pp2_kernel<T, AK, BK, EPI>;
+  (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  int nb = 0;
+  if (p.bias_mode == 1) nb = (p.n_bias > 0 ? p.batch0 : 1) * p.N;
+  const size_t lds = (size_t)PP_NSLOT * PP_SLOT + (size_t)nb * sizeof(float);
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(512), lds, st, p);
+}
+
 template <typename T, bool AK, bool BK, class C>
 static void launch_persist_cfg(const GemmParams& p, int blocks, hipStream_t st, int cfg) {
   int epi = (p.beta != 0.f ? 1 : 0) | (p.aux != nullptr ? 2 : 0);
   if (epi == 0 && p.relu) epi = 4;
+  if (cfg == 45) {
+    switch (epi) {
+      case 0: launch_pp2_epi<T, AK, BK, 0>(p, blocks, st); break;
+      case 1: launch_pp2_epi<T, AK, BK, 1>(p, blocks, st); break;
+      case 2: launch_pp2_epi<T, AK, BK, 2>(p, blocks, st); break;
+      case 3: launch_pp2_epi<T, AK, BK, 3>(p, blocks, st); break;
+      default: launch_pp2_epi<T, AK, BK, 4>(p, blocks, st); break;
+    }
+    return;
+  }
   if (cfg == 43) {
     switch (epi) {
       case 0: launch_pp_epi<T, AK, BK, 0>(p, blocks, st); break;
@@ -1005,16 +1243,17 @@ int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int 
                   d->M % 256 == 0 && d->N % 256 == 0 && d->K % 64 == 0 && d->K >= 128 &&
                   p.c_vec8 && p.c_vec4 && p.bias_mode != 2 && nbias <= kPersistBias;
   if (!ok) return 0;
-  if (forced == 40 || forced == 43) return forced;
+  if (forced == 40 || forced == 43 || forced == 45) return forced;
   if (forced != 0 || env == 0) return 0;
-  if (env == 40 || env == 43) return env;
+  if (env == 40 || env == 43 || env == 45) return env;
   // default: the ping-pong kernel (cfg 43) wherever the launch has at least 1.5 tiles per CU
   // (below that the 160x256 / split tiles of the one-block-per-tile kernel quantise better: NT
   // 19200x512x2048 53 vs 68 us).  cfg 40 beat the one-block-per-tile kernel on every batched
   // step shape by 9-20 % (profiles/r04/gemm_persist_vs_vendor_a.jsonl); cfg 43 beats cfg 40 by
-  // 14-25 % on the same shapes (profiles/r05/gemm_pp_vs_persist.txt)
+  // 14-25 % on the same shapes (profiles/r05/step_ab_persist40_vs_pp43.txt), and cfg 45 (32-MFMA phases) beats cfg 43 in the step: 4.266 ->
+  // 4.193 ms, NT 0.91 -> 0.87, NN 0.87 -> 0.81 ms/step (profiles/r05/step_ab_pp43_vs_pp45.txt)
   const long W = (long)(d->M / 256) * (d->N / 256) * batch0 * (d->batch1 < 1 ? 1 : d->batch1);
-  return W * 2 >= 3L * num_cus() ? 43 : 0;
+  return W * 2 >= 3L * num_cus() ? 45 : 0;
 }
 
 }  // namespace jmt

@@ -16,15 +16,15 @@ import re
 import sqlite3
 from collections import defaultdict
 
-MANGLED = re.compile(r"gemm_(?:persist3?_|pp_split_|pp_)?kernel.*?Lb([01])ELb([01])E")
-DEMANGLED = re.compile(r"gemm_(?:persist3?_|pp_split_|pp_)?kernel<.*?(true|false), (true|false),")
+MANGLED = re.compile(r"gemm_(?:persist3?_|pp_split_|pp2?_)?kernel.*?Lb([01])ELb([01])E")
+DEMANGLED = re.compile(r"gemm_(?:persist3?_|pp_split_|pp2?_)?kernel<.*?(true|false), (true|false),")
 
 
 # ROCm 7.2's demangler prints gemm_persist_kernel<__bf16, AK, BK, ...> as
 # "gemm_persist_kernel<bool _Accum, bool, E, BK, ..." — the A majorness is lost.  Every
 # persistent launch has a K-major A in practice (the weight gradients, A MN-major, are split-K,
 # which the persistent kernel does not take: gemm_persist.hip persist_choice), so BK decides.
-BROKEN_PERSIST = re.compile(r"gemm_(?:persist3?|pp)_kernel<bool _Accum, bool, E, (true|false),")
+BROKEN_PERSIST = re.compile(r"gemm_(?:persist3?|pp2?)_kernel<bool _Accum, bool, E, (true|false),")
 # the split-K ping-pong kernel (cfg 44) takes the weight gradients (A MN-major): B decides too
 BROKEN_SPLIT = re.compile(r"gemm_pp_split_kernel<bool _Accum, bool, E, (true|false),")
 

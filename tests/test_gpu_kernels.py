@@ -195,7 +195,7 @@ def test_gemm_kconcat_and_pointer_tables(dt):
     assert (dW - ref).abs().max().item() <= _tol(dt, M) * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("cfg", [40, 43])
+@pytest.mark.parametrize("cfg", [40, 43, 45])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 def test_gemm_persistent(cfg, ak, bk):
     """gemm_persist_kernel (csrc/gemm_persist.hip: one block per CU walks whole 256x256 tiles
@@ -291,7 +291,8 @@ def test_gemm_pingpong_bit_identical_to_persistent(ak, bk):
     pieces on a counted-vmcnt schedule, the epilogue in two halves) accumulates every output in
     the same k order as cfg 40: bit-identical C on step shapes with several items per block
     (item boundaries inside the DMA stream), beta * C, the ReLU mask, bias tables — repeated
-    launches (a missed wait shows as a difference that comes and goes)."""
+    launches (a missed wait shows as a difference that comes and goes).  Also cfg 45, the same
+    schedule with one 32-MFMA phase per k-half (half the barriers per K-tile)."""
     from jmt import _lib
     lib = _lib.load()
     g = torch.Generator(device=DEV).manual_seed(43)
@@ -306,7 +307,7 @@ def test_gemm_pingpong_bit_identical_to_persistent(ak, bk):
         C0 = torch.randn(nb, M, N, device=DEV, generator=g).to(bf)
         aux = torch.randn(nb, M, N, device=DEV, generator=g).to(bf) if use_aux else None
         outs = {}
-        for cfg in (40, 43, 43, 43):
+        for cfg in (40, 43, 43, 43, 45, 45, 45):
             C = C0.clone()
             lib.jmt_gemm_set_debug(cfg << 8)
             try:
@@ -318,9 +319,10 @@ def test_gemm_pingpong_bit_identical_to_persistent(ak, bk):
             finally:
                 lib.jmt_gemm_set_debug(0)
             outs.setdefault(cfg, []).append(C)
-        for C in outs[43]:
-            assert torch.equal(C, outs[40][0]), (M, N, K, nb, beta, use_aux,
-                                                 int((C != outs[40][0]).sum()))
+        for cfg in (43, 45):
+            for C in outs[cfg]:
+                assert torch.equal(C, outs[40][0]), (cfg, M, N, K, nb, beta, use_aux,
+                                                     int((C != outs[40][0]).sum()))
         ref = (Al[0] @ Bl_t.transpose(1, 2)[0]) + bias[0] + beta * C0[0].float()
         if use_aux:
             ref = torch.where(aux[0].float() > 0, ref, torch.zeros_like(ref))
