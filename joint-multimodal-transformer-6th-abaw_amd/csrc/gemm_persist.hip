@@ -492,17 +492,15 @@ __device__ __forceinline__ void wait_vm_le(int n) {
 constexpr int PP_STK = 24;
 __device__ uint64_t g_pp_stamps[8 * PP_STK * 4 * 8];
 
-// SPL: 0 the 16-bit C epilogue (persist_epilogue, EPI), 1 split-K fp32 slabs (pp_slab_epilogue),
-// 2 slabs + the A row sums (dbias_ws)
-template <typename T, bool AK, bool BK, int EPI, int GRP, int MODE = 0, int SPL = 0>
+template <typename T, bool AK, bool BK, int EPI, int GRP, int MODE = 0>
 __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, const char* smem,
                                        const float* bias_lds, int nm, int W) {
   using C = CfgPP;
   typedef typename Frag16<T>::t F;
-  // epilogue VMEM operations per wave: 16-B stores of paired 16-bit sub-tiles, or of fp32
-  // sub-tiles (+ one row-sum store per half), and the beta * C / mask loads
-  constexpr int NST = SPL ? C::TM * C::TN + (SPL == 2 ? 2 : 0) : C::TM * (C::TN / 2);
-  constexpr int NLD = SPL ? 0 : ((EPI & 1) ? C::TM * C::TN : 0) + ((EPI & 2) ? C::TM * C::TN : 0);
+  // epilogue VMEM operations per wave: 16-B stores of paired 16-bit sub-tiles and the
+  // beta * C / mask loads
+  constexpr int NST = C::TM * (C::TN / 2);
+  constexpr int NLD = ((EPI & 1) ? C::TM * C::TN : 0) + ((EPI & 2) ? C::TM * C::TN : 0);
   constexpr int SUB = (GRP + PP_D) & 1;                    // parity of this group's pieces
   // VMEM operations younger than the wave's last piece of k-half g at its deadline, away from
   // the stream's end: its pieces of the load intervals (4g + 2 + SUB - PP_D, 4g - 2 + GRP]
@@ -518,16 +516,7 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
   const int dbg = MODE ? p.dbg : 0;
   const int wn = wl;
   const int G = gridDim.x;
-  // K-tiles of this block's items (split-K items differ by one K-tile at most)
-  int nT = nm * (p.K >> 6);
-  if (SPL && p.splits > 1) {
-    PWalk w = pwalk_init(p, blockIdx.x, W, G);
-    nT = 0;
-    for (int k = 0; k < nm; ++k) {
-      if (k) pwalk_next(p, w);
-      nT += pwalk_item(p, w).len;
-    }
-  }
+  const int nT = nm * (p.K >> 6);                          // K-tiles of this block's items
   const int npieces = 8 * nT;
   const int ins0 = SUB * 8 + 2 * wl;
 
@@ -651,7 +640,6 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
   PWalk cur_w = pwalk_init(p, blockIdx.x, W, G);
   PItem cur = pwalk_item(p, cur_w);
   int cur_left = cur.len;
-  float rsum[2] = {0.f, 0.f};                              // SPL 2: row sums of qm 0 / 1
   // epilogue of an item in two halves: rows 0-63 of the wave (quadrant qm = 0, final after
   // phase 2 of the item's last K-tile) in that K-tile's phase-3 load segment, rows 64-127 in the
   // next K-tile's phase-0 load segment — half the store burst per segment
@@ -659,17 +647,8 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
 
   // the stores of one epilogue half (h = 0: rows 0-63 of the wave, 1: rows 64-127) of item cur
   auto epilogue_half = [&](int h) {
-    if constexpr (SPL) {
-      if (h == 0) pp_slab_epilogue<C, 0, 4>(p, cur, acc, lane, wm, wn);
-      else pp_slab_epilogue<C, 4, 4>(p, cur, acc, lane, wm, wn);
-      if constexpr (SPL == 2) {                            // this wave's sub-tile (qm h, i wn)
-        pp_rowsum_store(p, cur, rsum[h], wm * C::WTM + 64 * h + 16 * wn, lane);
-        rsum[h] = 0.f;
-      }
-    } else {
-      if (h == 0) persist_epilogue<T, C, EPI, 0, 4>(p, cur, acc, bias_lds, lane, wm, wn, dbg & 64);
-      else persist_epilogue<T, C, EPI, 4, 4>(p, cur, acc, bias_lds, lane, wm, wn, dbg & 64);
-    }
+    if (h == 0) persist_epilogue<T, C, EPI, 0, 4>(p, cur, acc, bias_lds, lane, wm, wn, dbg & 64);
+    else persist_epilogue<T, C, EPI, 4, 4>(p, cur, acc, bias_lds, lane, wm, wn, dbg & 64);
   };
 
   const bool stamping = STAMP && blockIdx.x == 0 && lane == 0;
@@ -750,14 +729,6 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
             acc[4 * qm + i][j] = mfma16(fb[j], fa[i], acc[4 * qm + i][j]);   // C^T sub-tiles
       }
       __builtin_amdgcn_s_setprio(0);
-      if constexpr (SPL == 2) {
-        // A row sums of the wave's sub-tile (qm, i = wn), from the fragment the MFMAs just read
-        const float r = rsum[qm];
-        if (wn == 0) rsum[qm] = rowsum8(fa[0], r);
-        else if (wn == 1) rsum[qm] = rowsum8(fa[1], r);
-        else if (wn == 2) rsum[qm] = rowsum8(fa[2], r);
-        else rsum[qm] = rowsum8(fa[3], r);
-      }
       // rows stored by this phase's load segment restart at 0, here behind the MFMAs that do not
       // touch them (rows 0-63 after phase 3's epilogue half, rows 64-127 after phase 0's)
       if (pp == 3 && epA) {
@@ -823,15 +794,17 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p) {
 constexpr int P2_D = 10;
 static_assert(P2_D % 2 == 0 && P2_D <= 10, "pp2 deadline counts are derived for an even P2_D <= 10");
 
-template <typename T, bool AK, bool BK, int EPI, int GRP>
+// SPL: 0 the 16-bit C epilogue (persist_epilogue, EPI), 1 split-K fp32 slabs (pp_slab_epilogue),
+// 2 slabs + the A row sums (dbias_ws)
+template <typename T, bool AK, bool BK, int EPI, int GRP, int SPL = 0>
 __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, const char* smem,
                                         const float* bias_lds, int nm, int W) {
   using C = CfgPP;
   typedef typename Frag16<T>::t F;
   constexpr bool ISA = GRP == 1;                           // this group's operand: A (else B)
   constexpr bool KM = ISA ? AK : BK;
-  constexpr int NST = C::TM * (C::TN / 2);
-  constexpr int NLD = ((EPI & 1) ? C::TM * C::TN : 0) + ((EPI & 2) ? C::TM * C::TN : 0);
+  constexpr int NST = SPL ? C::TM * C::TN + (SPL == 2 ? 2 : 0) : C::TM * (C::TN / 2);
+  constexpr int NLD = SPL ? 0 : ((EPI & 1) ? C::TM * C::TN : 0) + ((EPI & 2) ? C::TM * C::TN : 0);
   constexpr int EPO = NST + NLD;                           // VMEM operations of one epilogue
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -839,8 +812,16 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
   constexpr int wm = GRP;
   const int wn = wl;
   const int G = gridDim.x;
-  const int nkt = p.K >> 6;
-  const int nT = nm * nkt;
+  // K-tiles of this block's items (split-K items differ by one K-tile at most)
+  int nT = nm * (p.K >> 6);
+  if (SPL && p.splits > 1) {
+    PWalk w = pwalk_init(p, blockIdx.x, W, G);
+    nT = 0;
+    for (int k = 0; k < nm; ++k) {
+      if (k) pwalk_next(p, w);
+      nT += pwalk_item(p, w).len;
+    }
+  }
   const int nh = 2 * nT;                                   // k-halves of the block's stream
   const int64_t ld = ISA ? p.lda : p.ldb;
   // per-lane byte offsets of this wave's instructions 2 wl, 2 wl + 1 of each half (h) of its
@@ -863,7 +844,7 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
   int iss_k = 0, iss_kt = 0, left = 0;
   const char* ps[2][2];
   auto set_stream = [&]() {
-    const int k0 = iss_kt * 64;
+    const int k0 = (iss_it.kt0 + iss_kt) * 64;
     int kl;
     const T* X = ISA ? operand_base<T>(p.a_ptr, p.a_mode, p.sA0, p.sA1, iss_it.b0, iss_it.b1,
                                        p.a_kseg, k0, kl)
@@ -878,7 +859,7 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
     left = seg - (kl >> 6);
   };
   auto next_ktile = [&]() {
-    if (++iss_kt == nkt) {
+    if (++iss_kt == iss_it.len) {
       iss_kt = 0;
       if (++iss_k < nm) {
         pwalk_next(p, iss_w);
@@ -903,7 +884,8 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
 #pragma unroll
       for (int e = 0; e < 2; ++e) glds16_at(ps[h][e] + kh, dst + (8 * h + e) * 1024);
   };
-  auto first = [&](int m) { return m > 0 && m < nh && m % (2 * nkt) == 0; };
+  // epilogues issued in this phase's / the previous phase's load segment (deadline counts)
+  bool ep_cur = false, ep_prev = false;
   // k-half g retired by this wave (at phase g - 1); counts as in the header comment, rounded
   // down near the stream's end
   auto deadline = [&](int g) {
@@ -911,13 +893,13 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
     const int m = g - 1;
     if constexpr (GRP == 0) {
       // younger: its piece of k-half m + 2 (phase m) and phase m's epilogue
-      const int n = (m + 2 < nh ? 4 : 0) + (first(m) ? EPO : 0);
+      const int n = (m + 2 < nh ? 4 : 0) + (ep_cur ? EPO : 0);
       if (n == 4) wait_vmcnt<4>();
       else wait_vm_le(n);
     } else {
       // younger: its pieces of k-halves m + 2 (phase m - 1) and m + 3 (phase m)
       const int n = (m + 2 < nh ? 4 : 0) + (m + 3 < nh ? 4 : 0) +
-                    ((first(m - 1) ? 1 : 0) + (first(m) ? 1 : 0)) * EPO;
+                    ((ep_prev ? 1 : 0) + (ep_cur ? 1 : 0)) * EPO;
       if (n == 8) wait_vmcnt<8>();
       else wait_vm_le(n);
     }
@@ -950,22 +932,38 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
   F fa[8] = {}, fb[4] = {};
   PWalk cur_w = pwalk_init(p, blockIdx.x, W, G);
   PItem cur = pwalk_item(p, cur_w);
-  int cur_left = nkt;
+  int cur_left = cur.len;
+  float rsum[2] = {0.f, 0.f};                              // SPL 2: row sums of sub-tiles wn, wn + 4
+  auto epilogue = [&]() {
+    if constexpr (SPL) {
+      pp_slab_epilogue<C, 0, 8>(p, cur, acc, lane, wm, wn);
+      if constexpr (SPL == 2) {
+        pp_rowsum_store(p, cur, rsum[0], wm * C::WTM + 16 * wn, lane);
+        pp_rowsum_store(p, cur, rsum[1], wm * C::WTM + 64 + 16 * wn, lane);
+        rsum[0] = rsum[1] = 0.f;
+      }
+    } else {
+      persist_epilogue<T, C, EPI>(p, cur, acc, bias_lds, lane, wm, wn);
+    }
+  };
   for (int t = 0; t < nT; ++t) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int m = 2 * t + ks;
       // ---- load segment
+      ep_prev = ep_cur;
+      ep_cur = false;
       if (ks == 0) {
         if (cur_left == 0) {                               // previous item done: its epilogue
-          persist_epilogue<T, C, EPI>(p, cur, acc, bias_lds, lane, wm, wn);
+          epilogue();
+          ep_cur = true;
 #pragma unroll
           for (int i = 0; i < C::TM; ++i)
 #pragma unroll
             for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           pwalk_next(p, cur_w);
           cur = pwalk_item(p, cur_w);
-          cur_left = nkt;
+          cur_left = cur.len;
         }
         --cur_left;
       }
@@ -993,6 +991,12 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
+      if constexpr (SPL == 2) {                            // A row sums, sub-tiles wn and wn + 4
+        if (wn == 0) { rsum[0] = rowsum8(fa[0], rsum[0]); rsum[1] = rowsum8(fa[4], rsum[1]); }
+        else if (wn == 1) { rsum[0] = rowsum8(fa[1], rsum[0]); rsum[1] = rowsum8(fa[5], rsum[1]); }
+        else if (wn == 2) { rsum[0] = rowsum8(fa[2], rsum[0]); rsum[1] = rowsum8(fa[6], rsum[1]); }
+        else { rsum[0] = rowsum8(fa[3], rsum[0]); rsum[1] = rowsum8(fa[7], rsum[1]); }
+      }
       if constexpr (GRP == 0) deadline(m + 1);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -1000,7 +1004,7 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
     }
   }
   if constexpr (GRP == 0) __builtin_amdgcn_s_barrier();
-  persist_epilogue<T, C, EPI>(p, cur, acc, bias_lds, lane, wm, wn);
+  epilogue();
 }
 
 template <typename T, bool AK, bool BK, int EPI>
@@ -1024,7 +1028,7 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(GemmParams p) {
   else pp2_run<T, AK, BK, EPI, 1>(p, lbase, smem, bias_lds, nm, W);
 }
 
-// split-K form (cfg 44): items are (tile, split) — the weight-gradient GEMMs (M, N = features,
+// split-K form (cfg 44, on the cfg 45 schedule): items are (tile, split) — the weight-gradient GEMMs (M, N = features,
 // K = B x T rows: a few 256 x 256 tiles over a long K); fp32 partial slabs (+ the A row sums) for
 // splitk_reduce_kernel, which jmt_gemm launches next
 // (An in-launch reduction — the S blocks of a tile meeting at a per-tile counter, then each
@@ -1040,8 +1044,8 @@ __global__ __launch_bounds__(512) void gemm_pp_split_kernel(GemmParams p) {
   const int nm = (W - (int)blockIdx.x + G - 1) / G;
   if (nm <= 0 || p.K < 64) return;
   const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  if ((threadIdx.x >> 6) < 4) pp_run<T, AK, BK, 0, 0, 0, SPL>(p, lbase, smem, nullptr, nm, W);
-  else pp_run<T, AK, BK, 0, 1, 0, SPL>(p, lbase, smem, nullptr, nm, W);
+  if ((threadIdx.x >> 6) < 4) pp2_run<T, AK, BK, 0, 0, SPL>(p, lbase, smem, nullptr, nm, W);
+  else pp2_run<T, AK, BK, 0, 1, SPL>(p, lbase, smem, nullptr, nm, W);
 }
 
 // the persistent configuration (gemm_persist_kernel): cfg 40 = Cfg5's tile (128-B K-tiles, 2
