@@ -269,6 +269,7 @@ def parity_check(model, fc, audio, video, lv, la, cd, jm, fmt, Dv, nwin=2, k=1, 
 
 
 NORTH_STAR_TOL = {torch.float32: 1e-4, torch.bfloat16: 1e-2, torch.float16: 1e-2}
+RATIO_TO_EMULATED_BOUND = 1.25
 
 
 def north_star_key(cd) -> str:
@@ -299,6 +300,16 @@ def north_star_verdict(own: dict, cd, strict: dict = None) -> dict:
             "rounding_emulating_oracle_rel_to_spread": strict.get("pred_emulated_rel_to_spread"),
             "note": "relative to the spread no bf16 path is within 1e-2 on these weights: the "
                     "oracle with only its storage rounded to bf16 is at the value above"}
+        emu = strict.get("pred_emulated_rel_to_spread")
+        if emu:
+            # the GPU's spread-relative error over the rounding-emulating
+            # oracle's, tracked every round (bound 1.25: kernel changes must not drift it up)
+            ratio = strict["pred_abs_err_rel_to_spread"] / emu
+            out["conditioned"]["ratio_to_emulated"] = round(ratio, 3)
+            out["conditioned"]["ratio_bound"] = RATIO_TO_EMULATED_BOUND
+            out["conditioned"]["ratio_verdict"] = \
+                "pass" if ratio <= RATIO_TO_EMULATED_BOUND else "fail"
+            out["verdict_spread_relative"] = out["conditioned"]["ratio_verdict"]
     return out
 
 
@@ -338,7 +349,28 @@ def cpu_baseline(model_sd, fc_sd, audio, video, lv, la, steps=2):
                               "shared with the other GPU slots, so it is not used"}
 
 
-def launch_ranks(n: int, argv, script: str = None, backend: str = None) -> int:
+def visible_gpus():
+    """GPUs this process may use, WITHOUT initialising HIP (the launcher parent must not touch the
+    GPU before it starts its ranks): the first of HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES that is set, else the GPU nodes of the KFD topology in sysfs (nodes with
+    a non-zero gpu_id; CPU nodes have 0).  None when neither says (the ranks then check)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([d for d in v.split(",") if d.strip() not in ("", "-1")])
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for node in os.listdir(root):
+            with open(os.path.join(root, node, "gpu_id")) as f:
+                n += int(f.read().strip() or 0) != 0
+        return n
+    except (OSError, ValueError):
+        return None
+
+
+def launch_ranks(n: int, argv, script: str = None, backend: str = None,
+                 deadline_s: float = None) -> int:
     """Start `n` worker processes of `script` (this file) with torchrun's environment (RANK,
     LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT), one per GPU, and wait.
     Called before anything touches the GPU (torch.cuda.device_count() does not initialise it on
@@ -347,13 +379,15 @@ def launch_ranks(n: int, argv, script: str = None, backend: str = None) -> int:
     ONE bench line); every other line of every rank goes to stderr prefixed "[rank r]", as it
     comes (the ranks' logs, and a sign of life for long runs).  Returns the exit status: 0 only
     if every rank exited 0 and rank 0 printed a JSON line whose n_gpus is `n`; when one rank
-    fails the others are terminated (their own PIDs) after a grace period."""
+    fails the others are terminated (their own PIDs) after a grace period, and so are all of them
+    when the job outlives `deadline_s` (a rank hung in a collective; exit status 124).  The
+    parent never initialises HIP: the GPU count comes from visible_gpus()."""
     import socket
     import subprocess
     import threading
     backend = backend or os.environ.get("JMT_DIST_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()
-    if backend == "nccl" and ndev < n:
+    ndev = visible_gpus()
+    if backend == "nccl" and ndev is not None and ndev < n:
         print(f"bench.py --gpus {n}: only {ndev} GPU(s) visible; RCCL needs one rank per GPU "
               "(JMT_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs)", file=sys.stderr)
         return 2
@@ -386,6 +420,7 @@ def launch_ranks(n: int, argv, script: str = None, backend: str = None) -> int:
         t.start()
         threads.append(t)
     failed = None
+    t_end = None if deadline_s is None else time.time() + deadline_s
     while True:
         codes = [p.poll() for p in procs]
         bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
@@ -394,9 +429,14 @@ def launch_ranks(n: int, argv, script: str = None, backend: str = None) -> int:
             break
         if all(c == 0 for c in codes):
             break
+        if t_end is not None and time.time() > t_end:
+            failed = (next(r for r, c in enumerate(codes) if c is None), 124)
+            print(f"bench.py --gpus {n}: ranks still running after {deadline_s:.0f} s; "
+                  "terminating them", file=sys.stderr)
+            break
         time.sleep(0.2)
     if failed is not None:
-        deadline = time.time() + 30.0
+        deadline = time.time() + (0.0 if failed[1] == 124 else 30.0)
         while time.time() < deadline and any(p.poll() is None for p in procs):
             time.sleep(0.2)
         for p in procs:
@@ -426,6 +466,46 @@ def launch_ranks(n: int, argv, script: str = None, backend: str = None) -> int:
         return 1
     print(lines[-1], flush=True)
     return 0
+
+
+def _rank0_legs(args, cfg, cd, k, heads, layers, B, T, Da, Dv, model, fc, audio, video, lv, la,
+                rank, world, jcfg, model_sd0, fc_sd0):
+    """Rank 0's parity check and CPU baseline after the timed region (local CCC statistics: the
+    caller has taken the loss group away and restores it even if these raise)."""
+    parity = None
+    if rank == 0:
+        if (cfg["jm"], cfg["fmt"], cfg["fc"], k, heads, layers, Dv, Da) == \
+                ("TRANSFORMER", "FC", True, 1, 1, 1, 2048, 1024) and cd != torch.float32 and \
+                T == 300 and B >= 4:
+            # discriminative form (VERDICT r3 next #6): conditioned weights, the bench shape,
+            # every parameter gradient under the strict 16-bit bound (tests/parity.py)
+            from tests.parity import window_subset_check
+            torch.set_num_threads(cpu_threads()[0])
+            win = (0, B // 3, (2 * B) // 3, B - 1)
+            parity = window_subset_check(cd, B=B, T=T, win=win, perturb=args.parity_perturb)
+            parity["reference"] = ("oracle/jmt_ref.py fp32 CPU on windows %s of a B=%d T=%d batch "
+                                   "(whole batch on the GPU), conditioned hash-init weights, "
+                                   "objective zero outside those windows" % (list(win), B, T))
+            parity["tolerance"] = ("min(5 %, 4 x the rounding-emulating oracle's error, floor "
+                                   "2u) per prediction set / parameter gradient")
+            if args.parity_perturb:
+                parity["perturbed"] = ("cross_attention_v.out_proj.weight x %g on the GPU"
+                                       % (1 + args.parity_perturb))
+            # north_star's own number on the bench's fixed-seed batch and its trained weights
+            own = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv,
+                               k=k, H=heads, L=layers)
+            parity["bench_weights"] = own
+            parity[north_star_key(cd)] = north_star_verdict(own, cd, parity)
+        else:
+            parity = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv,
+                                  k=k, H=heads, L=layers)
+            parity[north_star_key(cd)] = north_star_verdict(parity, cd)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3" and \
+            jcfg is None:
+        cpu = cpu_baseline(model_sd0, fc_sd0, audio, video, lv, la)
+
+    return parity, cpu
 
 
 def main():
@@ -474,8 +554,10 @@ def main():
 
     if "WORLD_SIZE" not in os.environ:
         if (args.gpus or 1) > 1:
-            # no torchrun around us: be the launcher (nothing has touched the GPU yet)
-            raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+            # no torchrun around us: be the launcher (nothing has touched the GPU yet); a job
+            # that outlives a generous bound on its own work (hung ranks) is terminated
+            budget = 600.0 + 2.0 * (args.steps + args.warmup + args.probe_steps)
+            raise SystemExit(launch_ranks(args.gpus, sys.argv[1:], deadline_s=budget))
     elif args.gpus is not None and int(os.environ["WORLD_SIZE"]) != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus "
                          f"{args.gpus}: one rank per GPU")
@@ -721,44 +803,15 @@ def main():
         print(f"rank {rank}/{world}: cuda:{local} backend {backend}, {B} windows, "
               f"{elapsed / args.steps * 1e3:.3f} ms/step (max over ranks), graph {use_graph}, "
               f"final loss {last_loss:.6f}", file=sys.stderr, flush=True)
-    parity = None
     # the parity and CPU legs run on rank 0 alone: the CCC losses inside them must use local
     # statistics (a loss group would all-gather with ranks that are not there)
     group = jdist.loss_group()
     jdist.set_loss_group(None)
-    if rank == 0 and not args.no_parity:
-        if (cfg["jm"], cfg["fmt"], cfg["fc"], k, heads, layers, Dv, Da) == \
-                ("TRANSFORMER", "FC", True, 1, 1, 1, 2048, 1024) and cd != torch.float32 and \
-                T == 300 and B >= 4:
-            # discriminative form: conditioned weights, the bench shape,
-            # every parameter gradient under the strict 16-bit bound (tests/parity.py)
-            from tests.parity import window_subset_check
-            torch.set_num_threads(cpu_threads()[0])
-            win = (0, B // 3, (2 * B) // 3, B - 1)
-            parity = window_subset_check(cd, B=B, T=T, win=win, perturb=args.parity_perturb)
-            parity["reference"] = ("oracle/jmt_ref.py fp32 CPU on windows %s of a B=%d T=%d batch "
-                                   "(whole batch on the GPU), conditioned hash-init weights, "
-                                   "objective zero outside those windows" % (list(win), B, T))
-            parity["tolerance"] = ("min(5 %, 4 x the rounding-emulating oracle's error, floor "
-                                   "2u) per prediction set / parameter gradient")
-            if args.parity_perturb:
-                parity["perturbed"] = ("cross_attention_v.out_proj.weight x %g on the GPU"
-                                       % (1 + args.parity_perturb))
-            # north_star's own number on the bench's fixed-seed batch and its trained weights
-            own = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv,
-                               k=k, H=heads, L=layers)
-            parity["bench_weights"] = own
-            parity[north_star_key(cd)] = north_star_verdict(own, cd, parity)
-        else:
-            parity = parity_check(model, fc, audio, video, lv, la, cd, cfg["jm"], cfg["fmt"], Dv,
-                                  k=k, H=heads, L=layers)
-            parity[north_star_key(cd)] = north_star_verdict(parity, cd)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3" and \
-            jcfg is None:
-        cpu = cpu_baseline(model_sd0, fc_sd0, audio, video, lv, la)
-
-    jdist.set_loss_group(group)
+    try:
+        parity, cpu = _rank0_legs(args, cfg, cd, k, heads, layers, B, T, Da, Dv, model, fc, audio,
+                                  video, lv, la, rank, world, jcfg, model_sd0, fc_sd0)
+    finally:
+        jdist.set_loss_group(group)
     if rank == 0:
         out = {
             "metric": "train windows/sec + CCC parity, B=64 T=300 A/V fusion, 1/2/4/8 MI355X",

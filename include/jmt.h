@@ -23,7 +23,9 @@
 extern "C" {
 #endif
 
-#define JMT_ABI_VERSION 6
+#define JMT_ABI_VERSION 7
+/* ABI 7 (round 6): jmt_attn_bwd with dq == NULL writes P and dS only (the 128-row kernel), and
+ * jmt_attn_dkdv takes k / dq (+ strides) and computes dQ = dS K as its third product. */
 /* ABI 6 (round 5): jmt_attn_bwd_km removed (the key-major P / dS hand-off measured slower than
  * jmt_attn_bwd + jmt_attn_dkdv); the split-K workspace holds the fp32 slabs only. */
 
@@ -191,6 +193,13 @@ int jmt_softmax_bwd(int p_dt, int ds_dt, int64_t rows, int n, const void* p, int
  *   P = exp(scale Q K^T - lse), writes p_out = P and ds_out = scale * P o (dO V^T - rowsum(dO o O))
  *   (N*H*Lq rows of ldp >= Lk, row (n*H + h)*Lq + l; columns [Lk, ldp) zero) and
  *   dq = ds K.  dK = ds^T Q and dV = P^T dO are left to jmt_gemm.
+ *   dq == NULL (ABI 7): P and ds only, by the 128-query-row kernel (no dQ accumulator: the whole
+ *   512-dim Q / dO rows of a wave stay in registers), in the TILE-MAJOR layout: the (n, h)
+ *   region of Lq * ldp values holds ldp / 32 key tiles, tile t = [Lq queries][32 keys]
+ *   (element ((n*H + h) * ldp / 32 + t) * Lq * 32 + l * 32 + c = key 32 t + c of query l);
+ *   ldp a multiple of 32 >= Lk (keys [Lk, 32 ceil(Lk / 32)) written as zeros, later tiles
+ *   untouched), (Lq + 128) ldp 16-bit values < 1 GiB; dq / sdq_* ignored.  dQ, dK and dV then
+ *   come from jmt_attn_dkdv with dq != NULL.
  * (ABI 3: replaces ABI 2's jmt_attn_fwd p_out/mt outputs, jmt_attn_mt_floats and
  * jmt_attn_bwd_dq.) */
 int jmt_attn_supported(int dt, int dh);
@@ -210,11 +219,16 @@ int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const void* go, i
  * columns, row stride ldp >= 128 ceil(Lk / 128): the kernel reads whole 128-key tiles; columns past
  * Lk only feed outputs that are not stored).  dO / Q / dK / dV seq-first views as jmt_attn_bwd's
  * operands (row stride s*_l, batch stride s*_n, head h at columns 512 h).  16-bit, dh = 512.
- * Replaces the two batched TN jmt_gemm calls (M = Lk, N = dh, K = Lq) of the same products. */
+ * Replaces the two batched TN jmt_gemm calls (M = Lk, N = dh, K = Lq) of the same products.
+ * ABI 7: when dq != NULL also dQ = dS K (k: the attention's K operand, a view like q; dq like
+ * dk, rows Lq), as 128-query items beside the 128-key dK / dV items of the same launch, and P /
+ * dS are read in the tile-major layout jmt_attn_bwd(dq = NULL) writes (the pair's contract);
+ * dS keys [0, 32 ceil(Lk / 32)) feed dQ. */
 int jmt_attn_dkdv(int dt, int N, int H, int Lq, int Lk, int dh, const void* p, const void* ds,
                   int64_t ldp, const void* go, int64_t sgo_l, int64_t sgo_n, const void* q,
-                  int64_t sq_l, int64_t sq_n, void* dk, int64_t sdk_l, int64_t sdk_n, void* dv,
-                  int64_t sdv_l, int64_t sdv_n, void* stream);
+                  int64_t sq_l, int64_t sq_n, const void* k, int64_t sk_l, int64_t sk_n, void* dk,
+                  int64_t sdk_l, int64_t sdk_n, void* dv, int64_t sdv_l, int64_t sdv_n, void* dq,
+                  int64_t sdq_l, int64_t sdq_n, void* stream);
 
 /* Fused attention over short sequences, the whole backward in one kernel (Lq, Lk <= 32, 16-bit,
  * dh = 512; the batch-axis self-attention of mm_transformers.py:119-146 at B = 32 and every

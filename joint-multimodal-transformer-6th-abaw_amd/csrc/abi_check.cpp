@@ -38,6 +38,7 @@ int main() {
   alignas(16) char buf[64];
   float* fnull = nullptr;
   void* misal = (void*)(buf + 1);
+  void* algn = (void*)buf;        // aligned, never dereferenced (the checks fail first)
 
   // GEMM: descriptor validation and the host planners
   jmt_gemm_desc d;
@@ -101,11 +102,21 @@ int main() {
                                             1, misal, 1, 1, misal, 1, 1, misal, 1, 1, fnull,
                                             misal, misal, 8, misal, 1, 1, 0.1f, nullptr));
   expect_err("attn_dkdv ldp", jmt_attn_dkdv(JMT_BF16, 2, 1, 300, 300, 512, misal, misal, 320,
-                                           misal, 512, 512, misal, 512, 512, misal, 512, 512,
-                                           misal, 512, 512, nullptr));
+                                           misal, 512, 512, misal, 512, 512, nullptr, 0, 0,
+                                           misal, 512, 512, misal, 512, 512, nullptr, 0, 0,
+                                           nullptr));
   expect_err("attn_dkdv head dim", jmt_attn_dkdv(JMT_BF16, 2, 1, 300, 300, 64, misal, misal, 384,
-                                                 misal, 512, 512, misal, 512, 512, misal, 512,
-                                                 512, misal, 512, 512, nullptr));
+                                                 misal, 512, 512, misal, 512, 512, nullptr, 0, 0,
+                                                 misal, 512, 512, misal, 512, 512, nullptr, 0,
+                                                 0, nullptr));
+  expect_err("attn_dkdv dq misaligned", jmt_attn_dkdv(JMT_BF16, 2, 1, 300, 300, 512, algn, algn,
+                                                      384, algn, 512, 512, algn, 512, 512, misal,
+                                                      512, 512, algn, 512, 512, algn, 512, 512,
+                                                      misal, 512, 512, nullptr));
+  expect_err("attn_bwd pds ldp", jmt_attn_bwd(JMT_BF16, 2, 1, 300, 300, 512, algn, 512, 512,
+                                              algn, 512, 512, algn, 512, 512, algn, 512, 512,
+                                              algn, 512, 512, fnull, algn, algn, 300, nullptr,
+                                              0, 0, 0.1f, nullptr));
   expect_err("small_attn_fwd null", jmt_small_attn_fwd(JMT_BF16, 4, 1, 6, 6, 512, nullptr, 512,
                                                        512, nullptr, 512, 512, nullptr, 512, 512,
                                                        nullptr, 512, 512, 0.1f, fnull, nullptr));

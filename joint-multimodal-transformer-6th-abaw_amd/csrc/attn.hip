@@ -589,6 +589,238 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_kernel(AttnBwdArgs p) {
   }
 }
 
+// ------------------------------------------------------------------ P / dS only (round 6)
+// The backward of the jmt_attn_dkdv path: P and dS for jmt_attn_dkdv, which computes dQ = dS K
+// as its third product, so this kernel keeps no dQ accumulator.  The freed registers hold the
+// WHOLE 512-dim Q and dO rows of a wave (16 fragments each, 128 VGPRs), so:
+//  * a block is 8 waves x 16 rows = 128 query rows (the dQ kernel above: 64) — every K / V tile
+//    staged into LDS feeds twice the rows, halving the L2 -> LDS fill per FLOP, which bounded it
+//    (~64 KiB per 32-key tile per 64-row block at ~4 TB/s chip-wide);
+//  * no exchange: each wave contracts all 512 dims itself (S and dP in one MFMA chain each), so
+//    no partial-score slots, no pair barrier — one barrier per tile (the K / V buffer turnover);
+//  * waves whose 16 rows all lie past Lq (the 44-row tail q-tile of L = 300) skip their MFMAs
+//    and stores (wave-uniform), so the tail costs what its rows need.
+// Per 32-key tile a wave reads the K and V tiles whole (64 KiB) and issues 64 MFMAs: the LDS
+// array (256 B/clk/CU) and the MFMA pipes are both at 2048 cycles per tile at 2 waves/SIMD.
+// P / dS leave by 16-B buffer stores, 64 contiguous bytes per row (range-checked rows: the count
+// is fixed, so the end-of-tile wait leaves this tile's 2 stores in flight and waits only for the
+// next tile's DMA).
+// LDS: 2 x (K 32 KiB + V 32 KiB) = 128 KiB.
+constexpr int AP_QT = 128;
+constexpr int AP_KT = 32;
+constexpr int AP_LDS = 4 * AP_KT * AT_ROWB;
+
+// DBG (ablations, timing only, wrong results; JMT_ATTN_PDS_DBG in the diagnostic build): 1 no
+// next-item row loads (stale Q / dO / O), 2 no MFMAs, 4 no softmax and no P / dS stores, 8 no
+// K / V DMA, 16 softmax computed but not stored, 32 nontemporal stores
+template <typename T, int DBG = 0>
+__global__ __launch_bounds__(512, 2) void attn_bwd_pds_kernel(AttnBwdArgs p) {
+  typedef typename Frag16<T>::t F;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int IMG = AP_KT * AT_ROWB;            // one K or V image (32 KiB)
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int nqt = (p.Lq + AP_QT - 1) / AP_QT;
+  const int nkt = (p.Lk + AP_KT - 1) / AP_KT;
+  int item, iend, istride;
+  item_range(p.nitems, item, iend, istride);
+  if (item >= iend) return;
+
+  int nh = item / nqt, n = nh / p.H, hd = nh % p.H, q0 = (item % nqt) * AP_QT;
+  const T* kb = (const T*)p.k + (int64_t)n * p.sk_n + hd * AT_DH;
+  const T* vb = (const T*)p.v + (int64_t)n * p.sv_n + hd * AT_DH;
+
+  // lane (li, g): row q0 + 16 w + li, dims 32 ks + 8 g .. +7 of fragment ks
+  // The next item's Q / dO go out right after the last tile's MFMAs, its O (Delta only) after
+  // the item's last softmax.
+  F qf[16], df[16], of[16];
+  auto load_qd = [&](int n_, int hd_, int q0_) {
+    const int64_t qc_ = min(q0_ + 16 * w + li, p.Lq - 1), coff = (int64_t)hd_ * AT_DH + 8 * g;
+    const T* qrow = (const T*)p.q + (int64_t)n_ * p.sq_n + qc_ * p.sq_l + coff;
+    const T* drow = (const T*)p.go + (int64_t)n_ * p.sgo_n + qc_ * p.sgo_l + coff;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      qf[ks] = *(const F*)(qrow + 32 * ks);
+      df[ks] = *(const F*)(drow + 32 * ks);
+    }
+  };
+  auto load_o = [&](int n_, int hd_, int q0_) {
+    const int64_t qc_ = min(q0_ + 16 * w + li, p.Lq - 1), coff = (int64_t)hd_ * AT_DH + 8 * g;
+    const T* orow = (const T*)p.o + (int64_t)n_ * p.so_n + qc_ * p.so_l + coff;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) of[ks] = *(const F*)(orow + 32 * ks);
+  };
+  load_qd(n, hd, q0);
+  load_o(n, hd, q0);
+  int buf = 0;
+  stage_rows<T, AP_KT, 8, true>(smem, kb, p.sk_l, 0, p.Lk);
+  stage_rows<T, AP_KT, 8, true>(smem + IMG, vb, p.sv_l, 0, p.Lk);
+
+  int kb4[4];                                     // ds_read_b128 lane bases (whole row)
+#pragma unroll
+  for (int m = 0; m < 4; ++m) kb4[m] = row_base(m, li, g, 0);
+
+  while (true) {
+    const int qr = q0 + 16 * w + li;
+    const int qc = min(qr, p.Lq - 1);
+    // wave-uniform (scalar: the branches on it are s_cbranch, not EXEC masks): any row in range
+    const bool wact = __builtin_amdgcn_readfirstlane(q0 + 16 * w) < p.Lq;
+    const int nxt = item + istride;
+    const bool more = nxt < iend;
+    const int nh2 = nxt / nqt, n2 = nh2 / p.H, hd2 = nh2 % p.H, q02 = (nxt % nqt) * AP_QT;
+    const T* kb2 = (const T*)p.k + (int64_t)n2 * p.sk_n + hd2 * AT_DH;
+    const T* vb2 = (const T*)p.v + (int64_t)n2 * p.sv_n + hd2 * AT_DH;
+
+    float delta;                                  // rowsum(dO o O) of row qr
+    {
+      float dp = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dp += (float)of[ks][e] * (float)df[ks][e];
+      delta = pl_pair_sum(dp);
+    }
+    const float lse2 = p.lse[(int64_t)nh * p.Lq + qc] * 1.4426950408889634f;
+    // P / dS of this (n, h), TILE-MAJOR: [key tile jt][query][32 keys] (64-B rows, ldp / 32
+    // tiles), so one store instruction writes 16 consecutive rows = 1 KiB contiguous.  Buffer
+    // resources over the (n, h) region; rows past Lq get an offset past its end and are dropped
+    // by the range check, so every wave issues the same 2 stores per tile.
+    const int64_t region = (int64_t)nh * p.Lq * p.ldp;
+    const int nbytes = (int)((int64_t)p.Lq * p.ldp * (int64_t)sizeof(T));
+    auto mk_rsrc = [&](void* base) {
+      const uint64_t ba = (uint64_t)(uintptr_t)((T*)base + region);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ba);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(ba >> 32));
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
+                                               __builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
+    };
+    const auto rs_p = mk_rsrc(p.pbuf);
+    const auto rs_ds = mk_rsrc(p.dsbuf);
+    const int rowoff = qr * AP_KT;                // elements (used for rows below Lq only)
+
+    wait_vmcnt<0>();                              // tile 0 and this item's rows landed
+    lds_barrier();                                // ... for every wave; the previous item's
+                                                  // buffers are free
+    // One 32-key tile; the last one (LAST) is peeled out of the loop: the next item's Q / dO
+    // loads issued inside the loop would be pending at its header for hipcc's wait insertion,
+    // which then put a vmcnt(0) before every tile's first MFMA — waiting for the tile's own
+    // freshly issued DMA (no load / compute overlap at all).
+    auto tile = [&](int j, auto last_c) {
+      constexpr bool LAST = decltype(last_c)::value;
+      const char* kimg = smem + buf * 2 * IMG;
+      const char* vimg = kimg + IMG;
+      char* nk = smem + (buf ^ 1) * 2 * IMG;      // tile j+1 (or the next item's tile 0)
+      if ((DBG & 8) == 0 && (!LAST || more)) {
+        const T* kbn = LAST ? kb2 : kb;
+        const T* vbn = LAST ? vb2 : vb;
+        const int k0n = LAST ? 0 : AP_KT * (j + 1);
+        stage_rows<T, AP_KT, 8, true>(nk, kbn, p.sk_l, k0n, p.Lk);
+        stage_rows<T, AP_KT, 8, true>(nk + IMG, vbn, p.sv_l, k0n, p.Lk);
+      }
+      // ---- scores s[kt][r] = <row qr, key 32 j + 16 kt + 4 g + r> and dP over all 512 dims
+      f32x4 s[2], d[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        d[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if ((DBG & 2) == 0 && wact) {   // k-step batches (K and V fragments of key subtiles 0, 1),
+                                      // double-buffered
+        F fa[4], fb[4];
+        auto batch = [&](F* dst, int ks) {
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            const int o = kb4[ks & 3] + 256 * (ks >> 2) + 16384 * kt;
+            dst[kt] = *(const F*)(kimg + o);
+            dst[2 + kt] = *(const F*)(vimg + o);
+          }
+        };
+        batch(fa, 0);
+#pragma unroll
+        for (int ks = 0; ks < 16; ks += 2) {
+          batch(fb, ks + 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            s[kt] = mfma16(fa[kt], qf[ks], s[kt]);
+            d[kt] = mfma16(fa[2 + kt], df[ks], d[kt]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (ks + 2 < 16) batch(fa, ks + 2);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            s[kt] = mfma16(fb[kt], qf[ks + 1], s[kt]);
+            d[kt] = mfma16(fb[2 + kt], df[ks + 1], d[kt]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if constexpr (LAST && (DBG & 1) == 0) {
+        if (more) load_qd(n2, hd2, q02);          // registers free after the MFMAs
+      }
+      if ((DBG & 4) == 0 && wact) {
+        const int kbase = AP_KT * j + 4 * g;
+        uint32_t pk[2][2][2];                     // [P / dS][kt][dword]: 4 keys of subtile kt
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          T pv4[4], ds4[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const bool in = kbase + 16 * kt + r < p.Lk;
+            const float pv = in ? __builtin_amdgcn_exp2f(s[kt][r] * p.scale_log2 - lse2) : 0.f;
+            pv4[r] = from_f<T>(pv);
+            ds4[r] = from_f<T>(p.scale * pv * (d[kt][r] - delta));
+          }
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            pk[0][kt][q] = ((const uint32_t*)pv4)[q];
+            pk[1][kt][q] = ((const uint32_t*)ds4)[q];
+          }
+        }
+        // subtiles 0 / 1 paired by v_permlane16_swap (store_acc_direct's scheme): lane g then
+        // holds the 8 consecutive keys 16 (g & 1) + 8 (g >> 1) .. +7 of the tile: 16 B per lane,
+        // a whole 64-B tile row per 4 lanes, 16 rows contiguous (row-major [q][ldp] stores of
+        // 32-B / 64-B row pieces took 3/4 of the kernel: 215 -> 57 us without stores,
+        // profiles/r06/pds_ablate.txt)
+        const int off = qr < p.Lq ? (rowoff + j * p.Lq * AP_KT + 16 * (g & 1) + 8 * (g >> 1)) *
+                                        (int)sizeof(T)
+                                  : 0x7ffffff0;
+        JMT_DCHECK(AP_KT * j + AP_KT <= p.ldp);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const auto r0 = __builtin_amdgcn_permlane16_swap(pk[a][0][0], pk[a][1][0], false, false);
+          const auto r1 = __builtin_amdgcn_permlane16_swap(pk[a][0][1], pk[a][1][1], false, false);
+          const u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
+          if constexpr ((DBG & 16) != 0) {
+            asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b128(v, a == 0 ? rs_p : rs_ds, off, 0,
+                                                   (DBG & 32) ? 2 : 0);
+          }
+        }
+      }
+      if constexpr (!LAST) {
+        // tile j+1 landed: the 2 stores issued after its DMA may stay in flight
+        if ((DBG & 20) == 0 && wact) wait_vmcnt<2>();
+        else wait_vmcnt<0>();
+        lds_barrier();                            // visible to every wave; buffer `buf` free
+      }
+      buf ^= 1;
+    };
+    for (int j = 0; j + 1 < nkt; ++j) tile(j, std::false_type{});
+    tile(nkt - 1, std::true_type{});
+    if (!more) break;
+    // after the loop, not in its last iteration: loaded inside, O would be a loop-carried value
+    // pinned over every tile (64 VGPRs: the kernel spilled, and each spill reload's vmcnt(0)
+    // waited for the tile's DMA right after issuing it)
+    if constexpr ((DBG & 1) == 0) load_o(n2, hd2, q02);
+    item = nxt; nh = nh2; n = n2; hd = hd2; q0 = q02; kb = kb2; vb = vb2;
+  }
+}
+
 template <typename K>
 static void set_lds(K fn, int bytes) {
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
@@ -724,11 +956,63 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
     return set_error(JMT_ERR_UNSUPPORTED, "jmt_attn_bwd: dtype %d / head dim %d not supported",
                      dt, dh);
   const void* ptrs[] = {go, o, q, k, v, p_out, ds_out, dq};
-  const int64_t strides[] = {sgo_l, sgo_n, so_l, so_n, sq_l, sq_n, sk_l, sk_n, sv_l, sv_n,
-                             sdq_l, sdq_n, ldp};
-  int rc = check_common("jmt_attn_bwd", N, H, Lq, Lk, ptrs, 8, strides, 13);
+  const int64_t strides[] = {sgo_l, sgo_n, so_l, so_n, sq_l, sq_n, sk_l, sk_n, sv_l, sv_n, ldp,
+                             sdq_l, sdq_n};
+  const bool pds = dq == nullptr;                 // P / dS only: dQ left to jmt_attn_dkdv
+  int rc = check_common("jmt_attn_bwd", N, H, Lq, Lk, ptrs, pds ? 7 : 8, strides, pds ? 11 : 13);
   if (rc != JMT_OK) return rc;
   JMT_CHECK_ARG(lse && ldp >= Lk, "jmt_attn_bwd: lse missing or ldp < Lk");
+  if (pds) {
+    JMT_CHECK_ARG(ldp >= (int64_t)(Lk + AP_KT - 1) / AP_KT * AP_KT && ldp % AP_KT == 0 &&
+                      (int64_t)(Lq + AP_QT) * ldp * 2 < (1LL << 30),
+                  "jmt_attn_bwd (dq = NULL): ldp must be a multiple of 32 covering Lk, and Lq "
+                  "rows of ldp 16-bit values must stay below 1 GiB");
+    AttnBwdArgs a = {};
+    a.go = go; a.o = o; a.q = q; a.k = k; a.v = v; a.lse = lse;
+    a.pbuf = p_out; a.dsbuf = ds_out; a.dq = nullptr;
+    a.sgo_l = sgo_l; a.sgo_n = sgo_n; a.so_l = so_l; a.so_n = so_n; a.sq_l = sq_l; a.sq_n = sq_n;
+    a.sk_l = sk_l; a.sk_n = sk_n; a.sv_l = sv_l; a.sv_n = sv_n;
+    a.ldp = ldp;
+    a.Lq = Lq; a.Lk = Lk; a.H = H;
+    a.scale = scale;
+    a.scale_log2 = scale * 1.4426950408889634f;
+    a.nitems = ((Lq + AP_QT - 1) / AP_QT) * N * H;
+    const dim3 grid(persistent_grid(a.nitems));
+    hipStream_t st = as_stream(stream);
+#if JMT_DIAG
+    static const int dbg = getenv("JMT_ATTN_PDS_DBG") ? atoi(getenv("JMT_ATTN_PDS_DBG")) : 0;
+    if (dbg && dt == JMT_BF16) {
+#define JMT_PDS_DBG(D)                                                                       \
+  case D: {                                                                                  \
+    static bool once = (set_lds(attn_bwd_pds_kernel<__bf16, D>, AP_LDS), true);             \
+    (void)once;                                                                              \
+    hipLaunchKernelGGL((attn_bwd_pds_kernel<__bf16, D>), grid, dim3(512), (size_t)AP_LDS, st, \
+                       a);                                                                   \
+  } break;
+      switch (dbg) {
+        JMT_PDS_DBG(1) JMT_PDS_DBG(2) JMT_PDS_DBG(3) JMT_PDS_DBG(4) JMT_PDS_DBG(6)
+        JMT_PDS_DBG(7) JMT_PDS_DBG(8) JMT_PDS_DBG(15) JMT_PDS_DBG(16) JMT_PDS_DBG(32)
+        JMT_PDS_DBG(17) JMT_PDS_DBG(18)
+        default: return set_error(JMT_ERR_ARG, "JMT_ATTN_PDS_DBG=%d not built", dbg);
+      }
+#undef JMT_PDS_DBG
+      JMT_LAUNCH_CHECK("jmt_attn_bwd");
+      return JMT_OK;
+    }
+#endif
+    if (dt == JMT_BF16) {
+      static bool once = (set_lds(attn_bwd_pds_kernel<__bf16>, AP_LDS), true);
+      (void)once;
+      hipLaunchKernelGGL((attn_bwd_pds_kernel<__bf16>), grid, dim3(512), (size_t)AP_LDS, st, a);
+    } else {
+      static bool once = (set_lds(attn_bwd_pds_kernel<_Float16>, AP_LDS), true);
+      (void)once;
+      hipLaunchKernelGGL((attn_bwd_pds_kernel<_Float16>), grid, dim3(512), (size_t)AP_LDS, st,
+                         a);
+    }
+    JMT_LAUNCH_CHECK("jmt_attn_bwd");
+    return JMT_OK;
+  }
   AttnBwdArgs a = {};
   a.go = go; a.o = o; a.q = q; a.k = k; a.v = v; a.lse = lse;
   a.pbuf = p_out; a.dsbuf = ds_out; a.dq = dq;

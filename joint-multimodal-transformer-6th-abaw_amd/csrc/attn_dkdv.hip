@@ -52,10 +52,12 @@ struct AttnDkdvArgs {
   const void* ds;
   const void* go;
   const void* q;
+  const void* k;
   void* dk;
   void* dv;
-  int64_t ldp, sgo_l, sgo_n, sq_l, sq_n, sdk_l, sdk_n, sdv_l, sdv_n;
-  int Lq, Lk, H, nkt, nitems;
+  void* dq;
+  int64_t ldp, sgo_l, sgo_n, sq_l, sq_n, sk_l, sk_n, sdk_l, sdk_n, sdv_l, sdv_n, sdq_l, sdq_n;
+  int Lq, Lk, H, nkt, nqd, ipn, nitems;
 };
 
 // byte offset of 16-B chunk `c` of row `r` of a P / dS image
@@ -63,16 +65,32 @@ __device__ __forceinline__ int pimg_off(int r, int c) {
   return r * DK_PROW + ((c ^ ((r & 7) << 1)) << 4);
 }
 
-// item -> (n H + h, n, h, product (0: dV, 1: dK), first key)
+// byte offset of 16-B chunk `c` of row `r` of a dS image of the dQ product (128 query rows x 32
+// keys, 64-B rows): chunk c ^ ((r >> 2) & 3), so the two ds_read_b64 of a fragment (rows li of a
+// 16-row group, keys 4 g and 16 + 4 g) are conflict-free
+__device__ __forceinline__ int qimg_off(int r, int c) {
+  return r * 64 + ((c ^ ((r >> 2) & 3)) << 4);
+}
+
+// item -> (n H + h, n, h, product (0: dV, 1: dK, 2: dQ), first key (0, 1) or query (2), chunks).
+// Per (n, h): nkt dV items, nkt dK items (128-key tiles, the contraction over queries in 32-row
+// chunks), then nqd dQ items (128-query tiles, the contraction over keys in 32-key chunks).
 struct DkItem {
-  int nh, n, hd, role, k0;
+  int nh, n, hd, role, k0, nch;
 };
 __device__ __forceinline__ DkItem dk_decode(const AttnDkdvArgs& a, int it) {
   DkItem d;
-  const int t = it / a.nkt;
-  d.k0 = (it - t * a.nkt) * DK_KT;
-  d.nh = t >> 1;
-  d.role = t & 1;
+  d.nh = it / a.ipn;
+  const int r = it - d.nh * a.ipn;
+  if (r < 2 * a.nkt) {
+    d.role = r >= a.nkt;
+    d.k0 = (r - d.role * a.nkt) * DK_KT;
+    d.nch = (a.Lq + DK_QC - 1) / DK_QC;
+  } else {
+    d.role = 2;
+    d.k0 = (r - 2 * a.nkt) * DK_KT;
+    d.nch = (a.Lk + DK_QC - 1) / DK_QC;
+  }
   d.n = d.nh / a.H;
   d.hd = d.nh - d.n * a.H;
   return d;
@@ -87,6 +105,28 @@ __device__ __forceinline__ void dkdv_stage(char* st, const AttnDkdvArgs& a, cons
                                            int q0) {
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (d.role == 2) {
+    // dQ chunk: K rows q0 .. q0+31 (here q0 is the first KEY of the chunk) and the dS tile of the
+    // item's 128 queries x those 32 keys (one wave-instruction per wave: 16 rows of 64 B)
+    const char* kb = (const char*)((const T*)a.k + (int64_t)d.n * a.sk_n + d.hd * AT_DH);
+    const int ldk = (int)(a.sk_l * (int64_t)sizeof(T));
+#pragma unroll
+    for (int i = 0; i < DK_QC / 8; ++i) {
+      const int r = wu * (DK_QC / 8) + i;
+      const int src = min(q0 + r, a.Lk - 1);
+      const unsigned off = (unsigned)(lane ^ ((r & 7) << 1)) << 4;
+      glds16_asm(kb + (unsigned)(src * ldk) + off, st + r * AT_ROWB);
+    }
+    const int r = 16 * wu + (lane >> 2);                // dS image row (query d.k0 + r)
+    const int c = (lane & 3) ^ ((r >> 2) & 3);          // the logical chunk this lane's 16 B hold
+    const int src_row = min(d.k0 + r, a.Lq - 1);
+    JMT_DCHECK(src_row >= 0 && q0 + 8 * c + 8 <= a.ldp);
+    // tile-major dS (jmt_attn_bwd with dq = NULL): [key tile q0 / 32][query][32 keys]
+    const char* pb = (const char*)((const T*)a.ds + (int64_t)d.nh * a.Lq * a.ldp);
+    glds16_asm(pb + (unsigned)(((q0 >> 5) * a.Lq + src_row) * 64) + 16 * c,
+               st + DK_IMG + wu * 1024);
+    return;
+  }
   const char* rb;
   int ldb;
   if (d.role == 0) {
@@ -107,6 +147,14 @@ __device__ __forceinline__ void dkdv_stage(char* st, const AttnDkdvArgs& a, cons
   const int cs = (lane & 15) ^ ((r & 7) << 1);          // the logical chunk it holds
   const int src_row = min(q0 + r, a.Lq - 1);
   JMT_DCHECK(src_row >= 0 && d.k0 + 8 * cs + 8 <= a.ldp);
+  if (a.dq) {      // tile-major P / dS (jmt_attn_bwd with dq = NULL): [key tile][query][32 keys]
+    const char* pb = (const char*)((const T*)(d.role == 0 ? a.p : a.ds) +
+                                   (int64_t)d.nh * a.Lq * a.ldp);
+    glds16_asm(pb + (unsigned)((((d.k0 >> 5) + (cs >> 2)) * a.Lq + src_row) * 64) +
+                   16 * (cs & 3),
+               st + DK_IMG + wu * 1024);
+    return;
+  }
   const char* pb = (const char*)((const T*)(d.role == 0 ? a.p : a.ds) +
                                  (int64_t)d.nh * a.Lq * a.ldp + d.k0);
   glds16_asm(pb + (unsigned)(src_row * (int)(a.ldp * sizeof(T))) + 16 * cs,
@@ -138,7 +186,6 @@ __global__ __launch_bounds__(512, 2) void attn_dkdv_kernel(AttnDkdvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int nqc = (a.Lq + DK_QC - 1) / DK_QC;
   int item, iend, istride;
   item_range(a.nitems, item, iend, istride);
   if (item >= iend) return;
@@ -149,6 +196,10 @@ __global__ __launch_bounds__(512, 2) void attn_dkdv_kernel(AttnDkdvArgs a) {
 #pragma unroll
   for (int kg = 0; kg < 8; ++kg)
     pb[kg] = pimg_off(4 * g + (li >> 2), 2 * kg + ((li & 3) >> 1)) + 8 * (li & 1);
+  // dQ: dS fragment of query group qg = rows 16 qg + li, keys 4 g .. +3 (k-slots 0-3) and
+  // 16 + 4 g .. +3 (k-slots 4-7): the k-slot order of the transposed K-row reads
+  const int qb0 = qimg_off(li, g >> 1) + 8 * (g & 1);
+  const int qb1 = qimg_off(li, 2 + (g >> 1)) + 8 * (g & 1);
 
   // issue cursor: the chunk whose stage goes out next (runs DK_NS - 1 chunks ahead of the compute)
   int is_item = item, is_c = 0;
@@ -162,7 +213,7 @@ __global__ __launch_bounds__(512, 2) void attn_dkdv_kernel(AttnDkdvArgs a) {
       dkdv_stage<T>(smem + is_buf * DK_STAGE, a, is_d, DK_QC * is_c);
       after &= ~(15u << (4 * is_buf));
       ++inflight;
-      if (++is_c == nqc) {
+      if (++is_c == is_d.nch) {
         is_c = 0;
         is_item += istride;
         is_ok = is_item < iend;
@@ -183,7 +234,7 @@ __global__ __launch_bounds__(512, 2) void attn_dkdv_kernel(AttnDkdvArgs a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[kg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int c = 0; c < nqc; ++c) {
+    for (int c = 0; c < d.nch; ++c) {
       const char* cur = smem + buf * DK_STAGE;
       // this chunk's stage landed (the later stages and the output stores issued after it may
       // stay in flight), and every wave is done reading the buffer restaged below
@@ -192,17 +243,27 @@ __global__ __launch_bounds__(512, 2) void attn_dkdv_kernel(AttnDkdvArgs a) {
       lds_barrier();
       issue();
       F kf[8];
+      const int c0 = DK_QC * c;                         // first contraction index of the chunk
+      const int clen = d.role == 2 ? a.Lk : a.Lq;       // contraction length
+      if (d.role != 2) {
 #pragma unroll
-      for (int kg = 0; kg < 8; ++kg) {
-        const Hf lo = tr_read<Hf>(cur + DK_IMG + pb[kg]);
-        const Hf hi = tr_read<Hf>(cur + DK_IMG + pb[kg] + 16 * DK_PROW);
-        kf[kg] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        for (int kg = 0; kg < 8; ++kg) {
+          const Hf lo = tr_read<Hf>(cur + DK_IMG + pb[kg]);
+          const Hf hi = tr_read<Hf>(cur + DK_IMG + pb[kg] + 16 * DK_PROW);
+          kf[kg] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      } else {
+#pragma unroll
+        for (int qg = 0; qg < 8; ++qg) {
+          const Hf lo = *(const Hf*)(cur + DK_IMG + qb0 + 1024 * qg);
+          const Hf hi = *(const Hf*)(cur + DK_IMG + qb1 + 1024 * qg);
+          kf[qg] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
       }
-      const int q0 = DK_QC * c;
-      if (q0 + DK_QC > a.Lq) {                          // k-slot e holds query 16 (e >> 2) + 4 g + (e & 3)
+      if (c0 + DK_QC > clen) {   // k-slot e holds contraction index c0 + 16 (e >> 2) + 4 g + (e & 3)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const bool in = q0 + 16 * (e >> 2) + 4 * g + (e & 3) < a.Lq;
+          const bool in = c0 + 16 * (e >> 2) + 4 * g + (e & 3) < clen;
 #pragma unroll
           for (int kg = 0; kg < 8; ++kg) kf[kg][e] = in ? kf[kg][e] : from_f<T>(0.f);
         }
@@ -221,16 +282,18 @@ __global__ __launch_bounds__(512, 2) void attn_dkdv_kernel(AttnDkdvArgs a) {
       buf = buf == DK_NS - 1 ? 0 : buf + 1;
     }
 
-    // ---- outputs: lane = key k0 + 16 kg + li, dims 64 w + 16 t + 4 g + r; subtiles t, t + 1
-    // paired by v_permlane16_swap into 8 consecutive dims per lane (store_acc_direct's scheme)
+    // ---- outputs: lane = key (dQ: query) k0 + 16 kg + li, dims 64 w + 16 t + 4 g + r; subtiles
+    // t, t + 1 paired by v_permlane16_swap into 8 consecutive dims per lane (store_acc_direct's
+    // scheme)
     {
-      T* ob = d.role == 0 ? (T*)a.dv + (int64_t)d.n * a.sdv_n : (T*)a.dk + (int64_t)d.n * a.sdk_n;
-      const int64_t sl = d.role == 0 ? a.sdv_l : a.sdk_l;
+      T* ob = d.role == 0 ? (T*)a.dv + (int64_t)d.n * a.sdv_n
+            : d.role == 1 ? (T*)a.dk + (int64_t)d.n * a.sdk_n : (T*)a.dq + (int64_t)d.n * a.sdq_n;
+      const int64_t sl = d.role == 0 ? a.sdv_l : d.role == 1 ? a.sdk_l : a.sdq_l;
       ob += (int64_t)d.hd * AT_DH + (int64_t)d.k0 * sl;
       const uint64_t ba = (uint64_t)(uintptr_t)ob;
       const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)ba);
       const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(ba >> 32));
-      const int nrows = min(DK_KT, a.Lk - d.k0);
+      const int nrows = min(DK_KT, (d.role == 2 ? a.Lq : a.Lk) - d.k0);
       const int bytes = __builtin_amdgcn_readfirstlane((int)(nrows * sl * (int64_t)sizeof(T)));
       const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(((uint64_t)bhi << 32) | blo), 0, bytes, 0x00020000);
@@ -284,9 +347,10 @@ using namespace jmt;
 
 extern "C" int jmt_attn_dkdv(int dt, int N, int H, int Lq, int Lk, int dh, const void* p,
                              const void* ds, int64_t ldp, const void* go, int64_t sgo_l,
-                             int64_t sgo_n, const void* q, int64_t sq_l, int64_t sq_n, void* dk,
-                             int64_t sdk_l, int64_t sdk_n, void* dv, int64_t sdv_l,
-                             int64_t sdv_n, void* stream) {
+                             int64_t sgo_n, const void* q, int64_t sq_l, int64_t sq_n,
+                             const void* k, int64_t sk_l, int64_t sk_n, void* dk, int64_t sdk_l,
+                             int64_t sdk_n, void* dv, int64_t sdv_l, int64_t sdv_n, void* dq,
+                             int64_t sdq_l, int64_t sdq_n, void* stream) {
   if (N == 0 || Lk == 0) return JMT_OK;
   if (!((dt == JMT_BF16 || dt == JMT_F16) && dh == AT_DH))
     return set_error(JMT_ERR_UNSUPPORTED, "jmt_attn_dkdv: dtype %d / head dim %d not supported",
@@ -306,15 +370,27 @@ extern "C" int jmt_attn_dkdv(int dt, int N, int H, int Lq, int Lk, int dh, const
                     (int64_t)DK_KT * sdk_l * 2 < (1LL << 31) &&
                     (int64_t)DK_KT * sdv_l * 2 < (1LL << 31),
                 "jmt_attn_dkdv: dK / dV row stride out of range");
-  JMT_CHECK_ARG((int64_t)N * H * 2 * nkt < (1LL << 31), "jmt_attn_dkdv: too many items");
+  const int nqd = dq ? (Lq + DK_KT - 1) / DK_KT : 0;   // dQ items per (n, h)
+  if (dq) {
+    JMT_CHECK_ARG(k != nullptr && ((uintptr_t)k & 15) == 0 && ((uintptr_t)dq & 15) == 0 &&
+                      sk_l % 8 == 0 && sk_n % 8 == 0 && sdq_l % 8 == 0 && sdq_n % 8 == 0,
+                  "jmt_attn_dkdv: k / dq null, misaligned or strides not multiples of 8");
+    JMT_CHECK_ARG(sdq_l >= H * AT_DH && (int64_t)DK_KT * sdq_l * 2 < (1LL << 31) &&
+                      (int64_t)Lk * sk_l * 2 < (1LL << 31),
+                  "jmt_attn_dkdv: dQ / K row stride out of range");
+  }
+  JMT_CHECK_ARG((int64_t)N * H * (2 * nkt + nqd) < (1LL << 31), "jmt_attn_dkdv: too many items");
   JMT_CHECK_ARG((int64_t)Lq * sgo_l * 2 < (1LL << 31) && (int64_t)Lq * sq_l * 2 < (1LL << 31) &&
                     (int64_t)Lq * ldp * 2 < (1LL << 31),
                 "jmt_attn_dkdv: Lq rows of dO / Q / P exceed 2 GiB");
   AttnDkdvArgs a = {};
-  a.p = p; a.ds = ds; a.go = go; a.q = q; a.dk = dk; a.dv = dv;
+  a.p = p; a.ds = ds; a.go = go; a.q = q; a.k = k; a.dk = dk; a.dv = dv; a.dq = dq;
   a.ldp = ldp; a.sgo_l = sgo_l; a.sgo_n = sgo_n; a.sq_l = sq_l; a.sq_n = sq_n;
+  a.sk_l = sk_l; a.sk_n = sk_n;
   a.sdk_l = sdk_l; a.sdk_n = sdk_n; a.sdv_l = sdv_l; a.sdv_n = sdv_n;
-  a.Lq = Lq; a.Lk = Lk; a.H = H; a.nkt = nkt; a.nitems = N * H * 2 * nkt;
+  a.sdq_l = sdq_l; a.sdq_n = sdq_n;
+  a.Lq = Lq; a.Lk = Lk; a.H = H; a.nkt = nkt; a.nqd = nqd; a.ipn = 2 * nkt + nqd;
+  a.nitems = N * H * a.ipn;
   const dim3 grid(dkdv_grid(a.nitems));
   hipStream_t st = as_stream(stream);
   if (dt == JMT_BF16) {

@@ -98,7 +98,7 @@ _PROTOS = {
                                    c_i64, c_vp, c_i64, c_i64, c_f, c_vp]),
     "jmt_attn_dkdv": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_i64, c_vp,
                               c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
-                              c_i64, c_vp]),
+                              c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp]),
     "jmt_noop": (c_int, [c_vp]),
     "jmt_small_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64,
                                    c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
@@ -170,7 +170,7 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.jmt_abi_version() != 6:
+    if lib.jmt_abi_version() != 7:
         raise JMTError("libjmt_hip.so ABI version mismatch")
     cfg = int(os.environ.get("JMT_GEMM_CFG", "0"))   # development: force a GEMM pipeline config
     dbg = int(os.environ.get("JMT_GEMM_DBG", "0"))   # development: gemm.hip ablation flags

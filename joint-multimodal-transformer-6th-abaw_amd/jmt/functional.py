@@ -909,18 +909,25 @@ def attn_backward(saved, go, dq, dk, dv):
     if (fused and ops._attn_dkdv["on"] and _small_aligned(dk, kcol, cd)
             and _small_aligned(dv, vcol, cd)
             and ops.attn_dkdv_ok(N, H, Lq, Lk, dh, so_l, sq_l, dk.stride(0), dv.stride(0))):
-        # P and dS (rows of 128-key tiles) -> dK = dS^T Q and dV = P^T dO in one persistent kernel
+        # P and dS (rows of 128-key tiles) -> dK = dS^T Q and dV = P^T dO in one persistent
+        # kernel; with the 128-row P / dS kernel (default) dQ = dS K is that kernel's third
+        # product (JMT_ATTN_PDS=0: dQ inside the 64-row backward kernel instead)
         ldp = ops.attn_dkdv_ldp(Lk)
         P = torch.empty(N * H * Lq * ldp, dtype=cd, device=dev)
         dS = torch.empty(N * H * Lq * ldp, dtype=cd, device=dev)
+        pds = ops._attn_pds["on"] and _small_aligned(dq, qcol, cd) and _small_aligned(
+            k_src, kcol, cd) and ops.attn_pds_ok(
+            Lq, Lk, dq.stride(0), sk_l, H)
+        dq_args = (_ptr(dq, qcol), (dq.stride(0), dq.stride(1)))
         ops.attn_bwd(_dc(cd), N, H, Lq, Lk, dh, go.data_ptr(), (so_l, so_n),
                      o.data_ptr(), (o.stride(0), o.stride(1)),
                      _ptr(q_src, qcol), (sq_l, sq_n), _ptr(k_src, kcol), (sk_l, sk_n),
                      _ptr(v_src, vcol), (sv_l, sv_n), lse, P, dS, ldp,
-                     _ptr(dq, qcol), (dq.stride(0), dq.stride(1)), scale)
+                     *((None, (0, 0)) if pds else dq_args), scale)
         ops.attn_dkdv(_dc(cd), N, H, Lq, Lk, dh, P, dS, ldp, go.data_ptr(), (so_l, so_n),
                       _ptr(q_src, qcol), (sq_l, sq_n), _ptr(dk, kcol),
-                      (dk.stride(0), dk.stride(1)), _ptr(dv, vcol), (dv.stride(0), dv.stride(1)))
+                      (dk.stride(0), dk.stride(1)), _ptr(dv, vcol), (dv.stride(0), dv.stride(1)),
+                      *((_ptr(k_src, kcol), (sk_l, sk_n)) + dq_args if pds else ()))
         return
     bS = (H * Lq * ldS, Lq * ldS)
     dS = torch.empty(N * H * Lq * ldS, dtype=cd, device=dev)

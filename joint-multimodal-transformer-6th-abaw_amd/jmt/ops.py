@@ -264,20 +264,35 @@ def attn_fwd(dtype, N, H, Lq, Lk, dh, q_ptr, sq, k_ptr, sk, v_ptr, sv, o_ptr, so
 def attn_bwd(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k_ptr, sk, v_ptr, sv,
              lse, p, ds, ldp, dq_ptr, sdq, scale):
     """P = exp(scale Q K^T - lse) and dS = scale P o (dO V^T - rowsum(dO o O)) written to p / ds
-    (ldp), dQ = dS K."""
+    (ldp), dQ = dS K; dq_ptr None: P and dS only (the 128-row kernel; dQ from attn_dkdv)."""
     launch = lambda: _lib.call("jmt_attn_bwd", dtype, N, H, Lq, Lk, dh, go_ptr, sgo[0], sgo[1],
                                o_ptr, so[0], so[1], q_ptr, sq[0], sq[1], k_ptr, sk[0], sk[1],
                                v_ptr, sv[0], sv[1], lse.data_ptr(), p.data_ptr(), ds.data_ptr(),
                                ldp, dq_ptr, sdq[0], sdq[1], scale, stream())
-    # algorithmic: dP and dQ (the P recompute is not counted); bytes: dO, O, Q, K, V, dQ, lse and
-    # the P / dS rows handed to the dK / dV products
+    # algorithmic: two products per launch — dP and dQ, or (dq_ptr None) the S recompute and dP
+    # (cdna_hip_programming.md counts the recompute as one of the backward's five products);
+    # bytes: dO, O, Q, K, V, (dQ,) lse and the P / dS rows handed to attn_dkdv
     es = 4 if dtype == F32 else 2
+    nrow = 3 if dq_ptr is None else 4
     _hooked({"family": "attn_bwd", "flops": 4.0 * N * H * Lq * Lk * dh,
-             "bytes": float(N * H) * ((4 * Lq + 2 * Lk) * dh * es + 4 * Lq + 2 * Lq * ldp * es)},
-            launch)
+             "bytes": float(N * H) * ((nrow * Lq + 2 * Lk) * dh * es + 4 * Lq +
+                                      2 * Lq * ldp * es)}, launch)
 
 
 _attn_dkdv = {"on": os.environ.get("JMT_ATTN_DKDV", "1") != "0"}
+# the 128-row P / dS backward kernel with dQ as jmt_attn_dkdv's third product (round 6);
+# JMT_ATTN_PDS=0 keeps dQ in the 64-row backward kernel (A/B switch)
+_attn_pds = {"on": os.environ.get("JMT_ATTN_PDS", "1") != "0"}
+
+
+def attn_pds_ok(Lq, Lk, sdq_l, sk_l, H) -> bool:
+    """Host-side mirror of the dq = NULL checks of jmt_attn_bwd and the dQ checks of
+    jmt_attn_dkdv: P / dS rows of attn_dkdv_ldp(Lk) with 32-bit offsets over Lq + 128 rows, a
+    128-row dQ tile and Lk K rows within 32-bit byte offsets."""
+    ldp = attn_dkdv_ldp(Lk)
+    lim = 1 << 31
+    return ((Lq + 128) * ldp * 2 < lim and sdq_l >= H * 512 and 128 * sdq_l * 2 < lim
+            and Lk * sk_l * 2 < lim)
 
 
 def attn_dkdv_ldp(Lk: int) -> int:
@@ -298,18 +313,22 @@ def attn_dkdv_ok(N, H, Lq, Lk, dh, sgo_l, sq_l, sdk_l, sdv_l) -> bool:
 
 
 def attn_dkdv(dtype, N, H, Lq, Lk, dh, p, ds, ldp, go_ptr, sgo, q_ptr, sq, dk_ptr, sdk, dv_ptr,
-              sdv):
+              sdv, k_ptr=None, sk=(0, 0), dq_ptr=None, sdq=(0, 0)):
     """dV = P^T dO and dK = dS^T Q per (n, h) from attn_bwd's P / dS (ldp >= attn_dkdv_ldp(Lk));
-    one persistent kernel in place of two batched TN GEMMs (off with JMT_ATTN_DKDV=0)."""
+    with dq_ptr also dQ = dS K (k_ptr: the attention's K operand); one persistent kernel in place
+    of two (three) batched GEMMs (off with JMT_ATTN_DKDV=0)."""
     launch = lambda: _lib.call("jmt_attn_dkdv", dtype, N, H, Lq, Lk, dh, p.data_ptr(),
                                ds.data_ptr(), ldp, go_ptr, sgo[0], sgo[1], q_ptr, sq[0], sq[1],
-                               dk_ptr, sdk[0], sdk[1], dv_ptr, sdv[0], sdv[1], stream())
-    # algorithmic: the two products; bytes: P, dS (128-key tiles), dO and Q read once per head,
-    # dK and dV written
+                               k_ptr, sk[0], sk[1], dk_ptr, sdk[0], sdk[1], dv_ptr, sdv[0],
+                               sdv[1], dq_ptr, sdq[0], sdq[1], stream())
+    # algorithmic: the two (three) products; bytes: P, dS (128-key tiles), dO and Q read once per
+    # head, dK and dV written (+ K read per 128-query tile, dS again (32-key chunks), dQ written)
     es = 4 if dtype == F32 else 2
-    _hooked({"family": "attn_dkdv", "flops": 4.0 * N * H * Lq * Lk * dh,
+    nprod = 2 if dq_ptr is None else 3
+    extra = 0.0 if dq_ptr is None else (Lk + Lq) * dh * es + Lq * (-(-Lk // 32) * 32) * es
+    _hooked({"family": "attn_dkdv", "flops": 2.0 * nprod * N * H * Lq * Lk * dh,
              "bytes": float(N * H) * ((2 * Lq + 2 * Lk) * dh * es +
-                                      2 * Lq * attn_dkdv_ldp(Lk) * es)}, launch)
+                                      2 * Lq * attn_dkdv_ldp(Lk) * es + extra)}, launch)
 
 
 def attn_short_ok(dtype: int, dh: int, Lq: int, Lk: int) -> bool:

@@ -21,7 +21,7 @@ def header_functions():
 
 def test_library_loads_and_version():
     lib = _lib.load()
-    assert lib.jmt_abi_version() == 6
+    assert lib.jmt_abi_version() == 7
     assert lib.jmt_kernel_count() > 0
 
 

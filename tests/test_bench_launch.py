@@ -58,12 +58,63 @@ def test_launcher_rejects_wrong_n_gpus(capsys, monkeypatch):
     assert rc == 1 and out.strip() == "" and "n_gpus=1" in err
 
 
-def test_launcher_needs_one_gpu_per_rccl_rank(capsys):
+def test_launcher_needs_one_gpu_per_rccl_rank(capsys, monkeypatch):
     b = _bench()
-    import torch
-    n = torch.cuda.device_count() + 1
-    assert b.launch_ranks(n, [], script=FAKE, backend="nccl") == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    assert b.visible_gpus() == 2
+    assert b.launch_ranks(3, [], script=FAKE, backend="nccl") == 2
     assert "RCCL needs one rank per GPU" in capsys.readouterr().err
+
+
+def test_visible_gpus_reads_env_before_sysfs(monkeypatch):
+    b = _bench()
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "3,5,7")
+    assert b.visible_gpus() == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert b.visible_gpus() == 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "-1")
+    assert b.visible_gpus() == 0
+
+
+def test_launcher_parent_never_initialises_hip():
+    """the parent that starts the ranks must not be able to initialise HIP
+    (on ROCm torch.cuda.device_count() falls back to hipGetDeviceCount when amdsmi fails).  In a
+    child interpreter every torch.cuda entry that could reach HIP raises; launch_ranks with the
+    stand-in worker still succeeds and torch.cuda was never initialised."""
+    code = f"""
+import sys, torch
+def boom(*a, **k):
+    raise AssertionError("launcher parent touched torch.cuda")
+for name in ("device_count", "is_available", "init", "_lazy_init", "current_device",
+             "set_device", "synchronize", "get_device_properties"):
+    setattr(torch.cuda, name, boom)
+sys.path.insert(0, {REPO!r})
+import bench
+rc = bench.launch_ranks(2, [], script={FAKE!r}, backend="nccl")
+assert not torch.cuda.is_initialized()
+sys.exit(rc)
+"""
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="0,1")
+    env.pop("FAKE_RANK_FAIL", None)
+    env.pop("FAKE_RANK_NGPUS", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, text=True, capture_output=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 2
+
+
+def test_launcher_deadline_terminates_hung_ranks(capsys, monkeypatch):
+    """ranks that hang without exiting (e.g. in a collective) are terminated at the
+    job deadline and the launcher exits 124 with no bench line."""
+    b = _bench()
+    monkeypatch.delenv("FAKE_RANK_FAIL", raising=False)
+    monkeypatch.setenv("FAKE_RANK_HANG", "1")
+    rc = b.launch_ranks(2, [], script=FAKE, backend="gloo", deadline_s=3.0)
+    out, err = capsys.readouterr()
+    assert rc == 124 and out.strip() == ""
+    assert "still running after 3 s" in err
 
 
 def _run_bench(args, env_extra, timeout=240):

@@ -534,15 +534,18 @@ def test_fused_attention_fwd_vs_fp32(cd, Lq, Lk, N):
     assert (lse - lref).abs().max().item() <= 1e-3 * max(lref.abs().max().item(), 1.0)
 
 
+@pytest.mark.parametrize("pds", [False, True])
 @pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("Lq,Lk,N", [(300, 300, 3), (1, 6, 40), (70, 129, 2), (129, 1, 2),
-                                     (1024, 1024, 1),
+                                     (1024, 1024, 1), (257, 33, 3),
                                      # more (n, q-tile) items than CUs: the persistent grid
                                      (300, 300, 64), (70, 129, 200), (129, 1, 300)])
-def test_fused_attention_bwd_vs_fp32(cd, Lq, Lk, N):
+def test_fused_attention_bwd_vs_fp32(cd, Lq, Lk, N, pds):
     """jmt_attn_bwd (attn.hip): P recomputed from the forward's lse, dS and dQ vs an fp32
     reference from the same rounded inputs (P and dS are stored in the compute dtype; the
-    padding columns [Lk, ldp) of P and dS must be written as zeros)."""
+    padding columns [Lk, ldp) of P and dS must be written as zeros).  pds: dq = NULL, the
+    128-row P / dS kernel (round 6): the padding columns up to the 32-key tile are zeros, the
+    rest of the row and the dq buffer stay untouched."""
     E = 512
     g = torch.Generator(device=DEV).manual_seed(23)
     qkv = torch.randn(N, Lq, 3 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
@@ -557,15 +560,16 @@ def test_fused_attention_bwd_vs_fp32(cd, Lq, Lk, N):
                  (kv.stride(0), kv.stride(1)), o.data_ptr(), (o.stride(0), o.stride(1)), scale,
                  lse)
     go = torch.randn(Lq, N, E, device=DEV, generator=g).to(cd)
-    ldp = -(-Lk // 8) * 8
+    ldp = ops.attn_dkdv_ldp(Lk) if pds else -(-Lk // 8) * 8
     P = torch.full((N * Lq * ldp,), float("nan"), device=DEV, dtype=cd)
     dS = torch.full((N * Lq * ldp,), float("nan"), device=DEV, dtype=cd)
     dq = torch.full((N, Lq, 3 * E), float("nan"), device=DEV, dtype=cd).permute(1, 0, 2)
     ops.attn_bwd(dt, N, 1, Lq, Lk, E, go.data_ptr(), (go.stride(0), go.stride(1)), o.data_ptr(),
                  (o.stride(0), o.stride(1)), qp.data_ptr(), (qkv.stride(0), qkv.stride(1)),
                  kp.data_ptr(), (kv.stride(0), kv.stride(1)), vp.data_ptr(),
-                 (kv.stride(0), kv.stride(1)), lse, P, dS, ldp, dq[..., E:2 * E].data_ptr(),
-                 (dq.stride(0), dq.stride(1)), scale)
+                 (kv.stride(0), kv.stride(1)), lse, P, dS, ldp,
+                 None if pds else dq[..., E:2 * E].data_ptr(), (dq.stride(0), dq.stride(1)),
+                 scale)
     torch.cuda.synchronize()
     s = torch.einsum("lnd,knd->nlk", qp.float(), kp.float()) * scale
     pr = torch.softmax(s, -1)
@@ -573,10 +577,16 @@ def test_fused_attention_bwd_vs_fp32(cd, Lq, Lk, N):
     delta = (go.float() * o.float()).sum(-1).t().unsqueeze(-1)           # (N, Lq, 1)
     dsr = pr * (dp - delta) * scale
     dqr = torch.einsum("nlk,knd->lnd", dsr, kp.float())
-    Pg = P.view(N, Lq, ldp)
-    dSg = dS.view(N, Lq, ldp)
-    assert torch.isfinite(Pg.float()).all() and torch.isfinite(dSg.float()).all()
-    assert (Pg[..., Lk:] == 0).all() and (dSg[..., Lk:] == 0).all()
+    if pds:     # tile-major hand-off: (n, key tile, query, 32 keys) -> (n, query, key)
+        Pg = P.view(N, ldp // 32, Lq, 32).permute(0, 2, 1, 3).reshape(N, Lq, ldp)
+        dSg = dS.view(N, ldp // 32, Lq, 32).permute(0, 2, 1, 3).reshape(N, Lq, ldp)
+    else:
+        Pg = P.view(N, Lq, ldp)
+        dSg = dS.view(N, Lq, ldp)
+    lw = -(-Lk // 32) * 32 if pds else ldp        # columns the kernel writes
+    assert torch.isfinite(Pg[..., :lw].float()).all() and torch.isfinite(dSg[..., :lw].float()).all()
+    assert (Pg[..., Lk:lw] == 0).all() and (dSg[..., Lk:lw] == 0).all()
+    assert torch.isnan(Pg[..., lw:].float()).all() and torch.isnan(dSg[..., lw:].float()).all()
     u = 2.0 ** -8 if cd == torch.bfloat16 else 2.0 ** -11
     assert (Pg[..., :Lk].float() - pr).abs().max().item() <= 2 * u
     # dS error floor: Delta = rowsum(dO o O) from the 16-bit O (the cancellation dP - Delta is
@@ -584,21 +594,28 @@ def test_fused_attention_bwd_vs_fp32(cd, Lq, Lk, N):
     floor = 4 * u * scale * dp.abs().max().item()
     e_ds = (dSg[..., :Lk].float() - dsr).abs().max().item()
     assert e_ds <= 8 * u * dsr.abs().max().item() + floor, e_ds
+    if pds:
+        assert torch.isnan(dq.float()).all()
+        return
     e_dq = (dq[..., E:2 * E].float() - dqr).abs().max().item()
     assert e_dq <= 16 * u * dqr.abs().max().item() + floor * kp.float().abs().max().item(), e_dq
     assert torch.isnan(dq[..., :E].float()).all() and torch.isnan(dq[..., 2 * E:].float()).all()
 
 
+@pytest.mark.parametrize("with_dq", [False, True])
 @pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("Lq,Lk,N,H", [(300, 300, 3, 1), (1024, 1024, 1, 1), (77, 130, 2, 2),
                                        (33, 20, 3, 1), (1, 65, 2, 1), (129, 1, 2, 1),
+                                       (300, 45, 2, 1),
                                        # more (n, h, key-tile) items than CUs: persistent grid
                                        (300, 300, 64, 2), (40, 200, 100, 1)])
-def test_attn_dkdv_vs_fp32(cd, Lq, Lk, N, H):
+def test_attn_dkdv_vs_fp32(cd, Lq, Lk, N, H, with_dq):
     """jmt_attn_dkdv (attn_dkdv.hip): dV = P^T dO and dK = dS^T Q per (n, h) vs fp32 products of
     the same 16-bit inputs.  P / dS columns past Lk hold NaN (they may feed only keys that are
     not stored), outputs land in a packed (Lk, N, 3 E) buffer whose other columns must stay
-    untouched, and the ragged query / key tails cover the clamped rows and the dropped stores."""
+    untouched, and the ragged query / key tails cover the clamped rows and the dropped stores.
+    with_dq (ABI 7): also dQ = dS K (its third product: 128-query items, 32-key chunks, NaN in
+    the dS columns past Lk masked) into the first columns of a packed (Lq, N, 3 E) buffer."""
     E = 512 * H
     g = torch.Generator(device=DEV).manual_seed(31)
     ldp = ops.attn_dkdv_ldp(Lk)
@@ -611,9 +628,17 @@ def test_attn_dkdv_vs_fp32(cd, Lq, Lk, N, H):
     qv = qkv[..., :E]
     out = torch.full((N, Lk, 3 * E), 7.0, device=DEV, dtype=cd).permute(1, 0, 2)
     dk, dv = out[..., E:2 * E], out[..., 2 * E:]
+    kk = torch.randn(N, Lk, 2 * E, device=DEV, generator=g).to(cd).permute(1, 0, 2)
+    kv_ = kk[..., E:]
+    dqo = torch.full((N, Lq, 3 * E), 7.0, device=DEV, dtype=cd).permute(1, 0, 2)
+    dq = dqo[..., :E]
     st = lambda t: (t.stride(0), t.stride(1))
-    ops.attn_dkdv(ops.dt(qkv), N, H, Lq, Lk, 512, P, dS, ldp, go.data_ptr(), st(go),
-                  qv.data_ptr(), st(qkv), dk.data_ptr(), st(out), dv.data_ptr(), st(out))
+    # with dq: the tile-major P / dS layout of jmt_attn_bwd(dq = NULL)
+    tiled = lambda t: t.view(N * H, Lq, ldp // 32, 32).permute(0, 2, 1, 3).contiguous()
+    ops.attn_dkdv(ops.dt(qkv), N, H, Lq, Lk, 512, tiled(P) if with_dq else P,
+                  tiled(dS) if with_dq else dS, ldp, go.data_ptr(), st(go),
+                  qv.data_ptr(), st(qkv), dk.data_ptr(), st(out), dv.data_ptr(), st(out),
+                  *((kv_.data_ptr(), st(kk), dq.data_ptr(), st(dqo)) if with_dq else ()))
     torch.cuda.synchronize()
     Pr = P[..., :Lk].float().view(N, H, Lq, Lk)
     dSr = dS[..., :Lk].float().view(N, H, Lq, Lk)
@@ -628,6 +653,15 @@ def test_attn_dkdv_vs_fp32(cd, Lq, Lk, N, H):
         # fp32 accumulation of Lq products; the result rounded once to 16 bits
         assert err <= 2 * u * ref.abs().max().item() + 1e-6 * Lq, (err, ref.abs().max().item())
     assert (out[..., :E].float() == 7.0).all()
+    if with_dq:
+        kr = kv_.float().reshape(Lk, N, H, 512)
+        dqr = torch.einsum("nhqk,knhd->qnhd", dSr, kr).reshape(Lq, N, E)
+        assert torch.isfinite(dq.float()).all()
+        err = (dq.float() - dqr).abs().max().item()
+        assert err <= 2 * u * dqr.abs().max().item() + 1e-6 * Lk, (err, dqr.abs().max().item())
+        assert (dqo[..., E:].float() == 7.0).all()
+    else:
+        assert (dqo.float() == 7.0).all()
 
 
 @pytest.mark.parametrize("Lq,Lk,N", [(300, 300, 4), (70, 129, 3)])
@@ -648,8 +682,9 @@ def test_attention_backward_dkdv_matches_gemm_path(Lq, Lk, N):
         F.set_compute_dtype(None)
     go = torch.randn(Lq, N, E, device=DEV, generator=g).to(cd)
     res = []
-    for on in (True, False):
+    for on, pds in ((True, False), (False, False), (True, True)):
         ops._attn_dkdv["on"] = on
+        ops._attn_pds["on"] = pds
         try:
             dq = torch.zeros(N, Lq, 3 * E, device=DEV, dtype=cd).permute(1, 0, 2)
             dkv = torch.zeros(N, Lk, 2 * E, device=DEV, dtype=cd).permute(1, 0, 2)
@@ -658,10 +693,16 @@ def test_attention_backward_dkdv_matches_gemm_path(Lq, Lk, N):
             res.append((dq.float().clone(), dkv.float().clone()))
         finally:
             ops._attn_dkdv["on"] = True
+            ops._attn_pds["on"] = True
     assert torch.equal(res[0][0], res[1][0])
     ref = res[1][1]
     err = (res[0][1] - ref).abs().max().item()
     assert err <= 2 * 2.0 ** -8 * ref.abs().max().item(), err
+    # the 128-row P / dS kernel + dQ in attn_dkdv (default): its P / dS sum Delta and the scores
+    # in another order, so dQ / dK / dV agree within the 16-bit rounding of P and dS
+    for a, b in ((res[2][0], res[1][0]), (res[2][1], res[1][1])):
+        err = (a - b).abs().max().item()
+        assert err <= 4 * 2.0 ** -8 * b.abs().max().item(), err
 
 
 def test_attention_backward_dkdv_out_of_range_stride_takes_gemm_path():
