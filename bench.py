@@ -693,16 +693,30 @@ def main():
 
     run = step
     graphed = None
-    # N > 1 runs the bucketed step eagerly: its host issue time (host_issue_ms_per_eager_step,
-    # ~3 ms at c3) is below the GPU step, and eager is the N > 1 path the GPU tests have run.
-    # JMT_GRAPH_DIST=1 captures the RCCL all-reduces (per bucket, on the communication stream)
-    # and the CCC all-gather into the step graph too (tests/test_gpu_dist.py
-    # test_rccl_bucketed_step_sync_free_and_capturable, world size 1 only).
-    use_graph = args.graph and (world == 1 or os.environ.get("JMT_GRAPH_DIST", "0") == "1")
+    # N > 1: the step as hipGraph SEGMENTS with the collectives (CCC
+    # all-gather, per-bucket RCCL all-reduces, the final join) issued eagerly between them
+    # (jmt.graph.SegmentedStep): host issue is one graph launch per segment instead of the
+    # eager step's ~300 launches (host_issue_ms_per_eager_step, ~3 ms at c3), which a
+    # strong-scaling B = 8 per GPU step would not hide.  JMT_GRAPH_DIST=0: eager;
+    # JMT_GRAPH_DIST=1: the RCCL collectives captured into one whole-step graph
+    # (tests/test_gpu_dist.py test_rccl_bucketed_step_sync_free_and_capturable, world size 1).
+    gmode = os.environ.get("JMT_GRAPH_DIST", "segmented")
+    use_graph = args.graph and (world == 1 or gmode in ("1", "segmented"))
+    graph_kind = None
     if use_graph:
-        # the whole step as one hipGraph (jmt/graph.py): replay issues ~300 launches at once
-        graphed = GraphedStep(step).capture(warmup=1)
+        if world == 1 or gmode == "1":
+            # the whole step as one hipGraph (jmt/graph.py): replay issues ~300 launches at once
+            graphed = GraphedStep(step).capture(warmup=1)
+            graph_kind = "whole step"
+        else:
+            from jmt.graph import SegmentedStep
+            graphed = SegmentedStep(step).capture(warmup=1)
+            graph_kind = f"{len(graphed.segments)} segments, collectives eager between them"
         run = graphed.replay
+        torch.cuda.synchronize()
+        t_issue = time.perf_counter()
+        loss = run()                                # host time to issue one replayed step
+        host_issue_graph_ms = (time.perf_counter() - t_issue) * 1e3
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -836,6 +850,9 @@ def main():
             "cpu_baseline": cpu,
             "final_loss": round(last_loss, 6),
             "graph": bool(use_graph),
+            "graph_kind": graph_kind,
+            "host_issue_ms_per_graphed_step": (round(host_issue_graph_ms, 3) if use_graph
+                                               else None),
             "launcher": (os.environ.get("JMT_LAUNCHER", "torchrun") if world > 1 else None),
             "dist_backend": backend if world > 1 else None,
             "host_issue_ms_per_eager_step": round(host_issue_ms, 3),

@@ -612,9 +612,18 @@ constexpr int AP_LDS = 4 * AP_KT * AT_ROWB;
 
 // DBG (ablations, timing only, wrong results; JMT_ATTN_PDS_DBG in the diagnostic build): 1 no
 // next-item row loads (stale Q / dO / O), 2 no MFMAs, 4 no softmax and no P / dS stores, 8 no
-// K / V DMA, 16 softmax computed but not stored, 32 nontemporal stores
+// K / V DMA, 16 softmax computed but not stored, 32 nontemporal stores; 64 phase stamps
+// (s_memtime of block gridDim / 2, waves 0 and 4, into p.dq as a uint64 buffer of
+// 2 x 256 x 64: phases 8 t + {0 tile start, 1 DMA issued, 2 MFMAs issued, 3 softmax + stores
+// issued, 4 end wait, 5 barrier} of the block's first 31 tiles, 255 / 254 item start / end)
 template <typename T, int DBG = 0>
 __global__ __launch_bounds__(512, 2) void attn_bwd_pds_kernel(AttnBwdArgs p) {
+  int tcount = 0;
+  auto st = [&](int phase) {
+    if constexpr ((DBG & 64) != 0) {
+      if (tcount < 31) stamp<true>((uint64_t*)p.dq, 8 * tcount + phase);
+    }
+  };
   typedef typename Frag16<T>::t F;
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -655,8 +664,28 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_pds_kernel(AttnBwdArgs p) {
   load_qd(n, hd, q0);
   load_o(n, hd, q0);
   int buf = 0;
-  stage_rows<T, AP_KT, 8, true>(smem, kb, p.sk_l, 0, p.Lk);
-  stage_rows<T, AP_KT, 8, true>(smem + IMG, vb, p.sv_l, 0, p.Lk);
+  // K / V tile staging: wave w stages rows 4 w .. +3 of both images (one 1-KiB LDS-DMA row per
+  // wave-instruction).  Row offsets in 32-bit byte arithmetic from the (n, h) base (the host
+  // checks Lk rows fit) and the per-lane swizzled source offsets and LDS addresses computed once:
+  // stage_rows' 64-bit row products cost ~25 scalar instructions per DMA on the CU's one scalar
+  // unit (1-2.4k cycles of issue per tile, profiles/r06/pds_stamps*.txt)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  unsigned loff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) loff[i] = (unsigned)(lane ^ (((4 * wu + i) & 7) << 1)) << 4;
+  const int ldk = (int)(p.sk_l * (int64_t)sizeof(T)), ldv = (int)(p.sv_l * (int64_t)sizeof(T));
+  auto stage_tile = [&](int b, const T* kbase, const T* vbase, int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * wu + i;
+      const int src = min(k0 + r, p.Lk - 1);
+      const uint32_t dst = lbase + b * 2 * IMG + r * AT_ROWB;
+      glds16_at((const char*)kbase + (unsigned)(src * ldk) + loff[i], dst);
+      glds16_at((const char*)vbase + (unsigned)(src * ldv) + loff[i], dst + IMG);
+    }
+  };
+  stage_tile(0, kb, vb, 0);
 
   int kb4[4];                                     // ds_read_b128 lane bases (whole row)
 #pragma unroll
@@ -709,16 +738,12 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_pds_kernel(AttnBwdArgs p) {
     // freshly issued DMA (no load / compute overlap at all).
     auto tile = [&](int j, auto last_c) {
       constexpr bool LAST = decltype(last_c)::value;
+      st(0);
       const char* kimg = smem + buf * 2 * IMG;
       const char* vimg = kimg + IMG;
-      char* nk = smem + (buf ^ 1) * 2 * IMG;      // tile j+1 (or the next item's tile 0)
-      if ((DBG & 8) == 0 && (!LAST || more)) {
-        const T* kbn = LAST ? kb2 : kb;
-        const T* vbn = LAST ? vb2 : vb;
-        const int k0n = LAST ? 0 : AP_KT * (j + 1);
-        stage_rows<T, AP_KT, 8, true>(nk, kbn, p.sk_l, k0n, p.Lk);
-        stage_rows<T, AP_KT, 8, true>(nk + IMG, vbn, p.sv_l, k0n, p.Lk);
-      }
+      if ((DBG & 8) == 0 && (!LAST || more))
+        stage_tile(buf ^ 1, LAST ? kb2 : kb, LAST ? vb2 : vb, LAST ? 0 : AP_KT * (j + 1));
+      st(1);
       // ---- scores s[kt][r] = <row qr, key 32 j + 16 kt + 4 g + r> and dP over all 512 dims
       f32x4 s[2], d[2];
 #pragma unroll
@@ -758,6 +783,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_pds_kernel(AttnBwdArgs p) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      st(2);
       if constexpr (LAST && (DBG & 1) == 0) {
         if (more) load_qd(n2, hd2, q02);          // registers free after the MFMAs
       }
@@ -802,12 +828,16 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_pds_kernel(AttnBwdArgs p) {
           }
         }
       }
+      st(3);
       if constexpr (!LAST) {
         // tile j+1 landed: the 2 stores issued after its DMA may stay in flight
         if ((DBG & 20) == 0 && wact) wait_vmcnt<2>();
         else wait_vmcnt<0>();
+        st(4);
         lds_barrier();                            // visible to every wave; buffer `buf` free
+        st(5);
       }
+      ++tcount;
       buf ^= 1;
     };
     for (int j = 0; j + 1 < nkt; ++j) tile(j, std::false_type{});
@@ -964,9 +994,10 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
   JMT_CHECK_ARG(lse && ldp >= Lk, "jmt_attn_bwd: lse missing or ldp < Lk");
   if (pds) {
     JMT_CHECK_ARG(ldp >= (int64_t)(Lk + AP_KT - 1) / AP_KT * AP_KT && ldp % AP_KT == 0 &&
-                      (int64_t)(Lq + AP_QT) * ldp * 2 < (1LL << 30),
-                  "jmt_attn_bwd (dq = NULL): ldp must be a multiple of 32 covering Lk, and Lq "
-                  "rows of ldp 16-bit values must stay below 1 GiB");
+                      (int64_t)(Lq + AP_QT) * ldp * 2 < (1LL << 30) &&
+                      (int64_t)Lk * sk_l * 2 < (1LL << 31) && (int64_t)Lk * sv_l * 2 < (1LL << 31),
+                  "jmt_attn_bwd (dq = NULL): ldp must be a multiple of 32 covering Lk, Lq rows "
+                  "of ldp 16-bit values below 1 GiB and Lk K / V rows below 2 GiB");
     AttnBwdArgs a = {};
     a.go = go; a.o = o; a.q = q; a.k = k; a.v = v; a.lse = lse;
     a.pbuf = p_out; a.dsbuf = ds_out; a.dq = nullptr;
@@ -982,6 +1013,7 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
 #if JMT_DIAG
     static const int dbg = getenv("JMT_ATTN_PDS_DBG") ? atoi(getenv("JMT_ATTN_PDS_DBG")) : 0;
     if (dbg && dt == JMT_BF16) {
+      if (dbg & 64) a.dq = g_stamps;              // the stamps buffer (jmt_attn_set_stamps)
 #define JMT_PDS_DBG(D)                                                                       \
   case D: {                                                                                  \
     static bool once = (set_lds(attn_bwd_pds_kernel<__bf16, D>, AP_LDS), true);             \
@@ -992,7 +1024,7 @@ extern "C" int jmt_attn_bwd(int dt, int N, int H, int Lq, int Lk, int dh, const 
       switch (dbg) {
         JMT_PDS_DBG(1) JMT_PDS_DBG(2) JMT_PDS_DBG(3) JMT_PDS_DBG(4) JMT_PDS_DBG(6)
         JMT_PDS_DBG(7) JMT_PDS_DBG(8) JMT_PDS_DBG(15) JMT_PDS_DBG(16) JMT_PDS_DBG(32)
-        JMT_PDS_DBG(17) JMT_PDS_DBG(18)
+        JMT_PDS_DBG(17) JMT_PDS_DBG(18) JMT_PDS_DBG(64)
         default: return set_error(JMT_ERR_ARG, "JMT_ATTN_PDS_DBG=%d not built", dbg);
       }
 #undef JMT_PDS_DBG

@@ -458,8 +458,8 @@ void gemm_kernel(GemmParams p) {
                                  ka);
     const T* B = operand_base<T>(p.b_ptr, p.b_mode, p.sB0, p.sB1, cur.b0, cur.b1, p.b_kseg, k0,
                                  kb);
-    const int ka_lim = (p.a_mode == 2) ? min(p.a_kseg, ka + (cur.kend - k0)) : cur.kend;
-    const int kb_lim = (p.b_mode == 2) ? min(p.b_kseg, kb + (cur.kend - k0)) : cur.kend;
+    const int ka_lim = (p.a_mode >= 2) ? min(p.a_kseg, ka + (cur.kend - k0)) : cur.kend;
+    const int kb_lim = (p.b_mode >= 2) ? min(p.b_kseg, kb + (cur.kend - k0)) : cur.kend;
     char* base = smem + (nfull % C::S) * C::STAGE;
     stage_tile<T, AK, C::KB, C::BM, C::NT>(base, A, p.lda, p.M, cur.m0, ka_lim, ka);
     stage_tile<T, BK, C::KB, C::BN, C::NT>(base + IA, B, p.ldb, p.N, cur.n0, kb_lim, kb);
@@ -723,10 +723,23 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
     JMT_CHECK_ARG(((uintptr_t)d->a[i] & 15) == 0, "jmt_gemm: A[%d] not 16-B aligned", i);
   for (int i = 0; i < d->n_b; ++i)
     JMT_CHECK_ARG(((uintptr_t)d->b[i] & 15) == 0, "jmt_gemm: B[%d] not 16-B aligned", i);
+  JMT_CHECK_ARG(d->a_mode >= 0 && d->a_mode <= 3 && d->b_mode >= 0 && d->b_mode <= 3 &&
+                    d->c_mode >= 0 && d->c_mode <= 1, "jmt_gemm: bad operand mode");
   if (d->a_mode == 2) JMT_CHECK_ARG(d->a_kseg % BKE == 0 && d->a_kseg * d->n_a >= d->K,
                                     "jmt_gemm: A K-concat segment must be a multiple of %d", BKE);
   if (d->b_mode == 2) JMT_CHECK_ARG(d->b_kseg % BKE == 0 && d->b_kseg * d->n_b >= d->K,
                                     "jmt_gemm: B K-concat segment must be a multiple of %d", BKE);
+  // mode 3 (ABI 7): K-concat per batch entry, segment i of entry b0 at base[b0 * nseg + i]
+  const int nseg_a = d->a_mode == 3 && d->a_kseg > 0 ? (d->K + d->a_kseg - 1) / d->a_kseg : 1;
+  const int nseg_b = d->b_mode == 3 && d->b_kseg > 0 ? (d->K + d->b_kseg - 1) / d->b_kseg : 1;
+  if (d->a_mode == 3) JMT_CHECK_ARG(d->a_kseg > 0 && d->a_kseg % BKE == 0 &&
+                                        d->n_a >= batch0 * nseg_a && d->batch1 <= 1,
+                                    "jmt_gemm: A per-batch K-concat needs kseg a multiple of %d, "
+                                    "batch0 x ceil(K / kseg) pointers and batch1 = 1", BKE);
+  if (d->b_mode == 3) JMT_CHECK_ARG(d->b_kseg > 0 && d->b_kseg % BKE == 0 &&
+                                        d->n_b >= batch0 * nseg_b && d->batch1 <= 1,
+                                    "jmt_gemm: B per-batch K-concat needs kseg a multiple of %d, "
+                                    "batch0 x ceil(K / kseg) pointers and batch1 = 1", BKE);
   if (d->a_mode == 1) JMT_CHECK_ARG(d->n_a >= batch0, "jmt_gemm: A pointer table < batch0");
   if (d->b_mode == 1) JMT_CHECK_ARG(d->n_b >= batch0, "jmt_gemm: B pointer table < batch0");
   if (d->c_mode == 1) JMT_CHECK_ARG(d->n_c >= batch0, "jmt_gemm: C pointer table < batch0");
@@ -747,8 +760,10 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc; p.ldaux = d->ldaux;
   p.sA0 = d->sA0; p.sA1 = d->sA1; p.sB0 = d->sB0; p.sB1 = d->sB1; p.sC0 = d->sC0; p.sC1 = d->sC1;
   p.a_mode = d->a_mode; p.b_mode = d->b_mode; p.c_mode = d->c_mode;
-  p.a_kseg = d->a_mode == 2 ? d->a_kseg : 0;
-  p.b_kseg = d->b_mode == 2 ? d->b_kseg : 0;
+  p.a_kseg = d->a_mode >= 2 ? d->a_kseg : 0;
+  p.b_kseg = d->b_mode >= 2 ? d->b_kseg : 0;
+  if (d->a_mode == 3) p.sA0 = nseg_a;                 // operand_base: segments per entry
+  if (d->b_mode == 3) p.sB0 = nseg_b;
   p.M = d->M; p.N = d->N; p.K = d->K;
   p.batch0 = batch0; p.batch1 = batch1;
   p.alpha = d->alpha; p.beta = d->beta;

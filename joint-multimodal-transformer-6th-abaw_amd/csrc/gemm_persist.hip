@@ -534,8 +534,8 @@ __device__ __forceinline__ void pp_run(const GemmParams& p, uint32_t lbase, cons
   const int64_t da = (AK ? (int64_t)64 : (int64_t)64 * p.lda) * (int64_t)sizeof(T);   // K-tile
   const int64_t db = (BK ? (int64_t)64 : (int64_t)64 * p.ldb) * (int64_t)sizeof(T);
   const int64_t ha = da / 2, hb = db / 2;                                             // k-half
-  const int sega = p.a_mode == 2 ? p.a_kseg / 64 : 1 << 30;   // K-tiles per K-concat segment
-  const int segb = p.b_mode == 2 ? p.b_kseg / 64 : 1 << 30;
+  const int sega = p.a_mode >= 2 ? p.a_kseg / 64 : 1 << 30;   // K-tiles per K-concat segment
+  const int segb = p.b_mode >= 2 ? p.b_kseg / 64 : 1 << 30;
 
   // the issue stream: item iss_k, K-tile iss_kt of it, per-lane sources pa / pb of that K-tile
   PWalk iss_w = pwalk_init(p, blockIdx.x, W, G);
@@ -837,7 +837,7 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
     }
   const int64_t dk = (KM ? (int64_t)64 : (int64_t)64 * ld) * (int64_t)sizeof(T);   // K-tile
   const int64_t hk = dk / 2;                                                          // k-half
-  const int seg = (ISA ? p.a_mode : p.b_mode) == 2 ? (ISA ? p.a_kseg : p.b_kseg) / 64 : 1 << 30;
+  const int seg = (ISA ? p.a_mode : p.b_mode) >= 2 ? (ISA ? p.a_kseg : p.b_kseg) / 64 : 1 << 30;
 
   PWalk iss_w = pwalk_init(p, blockIdx.x, W, G);
   PItem iss_it = pwalk_item(p, iss_w);
@@ -1191,22 +1191,26 @@ bool pp_split_ok(int dt, int M, int N, int K, int splits) {
 }
 
 // the split count for cfg 44 on a launch of few tiles over a long K: enough (tile, split) items
-// for every CU, at least 4 K-tiles each; 0 when the shape has tiles enough without splitting,
-// and below 24 tiles, where each CU's 256 KiB fp32 slab outweighs the faster loop and the
-// 128 x 128 split plan stays ahead (TN 512 x 512 x 19200 b3: 62 vs 57 us, 512 x 2048: 70 vs 63;
-// 1024 x 512 b3 / b6, 1536 x 512 b3, 1024 x 3072: 6-10 % faster; profiles/r05/tn_pp_split_ab.txt)
+// for every CU, at least 4 K-tiles each; 0 when the shape has tiles enough without splitting.
+// Gate: the K-tiles each CU's item covers ((K / 64) x tiles / CUs, the work one 256 KiB fp32 slab
+// pays for) >= 27 — round 5 gated on >= 24 tiles, which at K = 19,200 is the same bound (28.1
+// K-tiles per CU at 24 tiles, 14 at the 12 of TN 512 x 512 b3: 62 vs 57 us on the 128 x 128 split
+// plan; 1024 x 512 b3 / b6, 1536 x 512 b3, 1024 x 3072: 6-10 % faster, profiles/r05/
+// tn_pp_split_ab.txt), but it also admits the 12-tile wgrads over K = 38,400 that the
+// cross-attentions' two uses of each module form (per-batch K-concat, grouped.py) and keeps
+// c4's 24 tiles over K = 16,384 (24 K-tiles per CU) off, where ADVICE r5 found cfg 44 slower.
 int pp_split_plan(int dt, int M, int N, int K, int batch) {
   // long K only: at realdata's K = 1024 rows a split is a few K-tiles, its pipeline prologue and
   // slab epilogue dominate (realdata 1.00 -> 1.22 ms/step; profiles/r05/cfg_gemm_ab.txt)
   if (dt == JMT_F32 || M % 256 || N % 256 || K % 64 || K < 8192) return 0;
   const long tiles = (long)(M / 256) * (N / 256) * batch;
   const int ncu = num_cus_persist();
-  static int min_tiles = -1;                  // development: JMT_GEMM_PPSPLIT_MIN_TILES
-  if (min_tiles < 0) {
-    const char* e = getenv("JMT_GEMM_PPSPLIT_MIN_TILES");
-    min_tiles = e ? atoi(e) : 24;
+  static int min_kt = -1;                     // development: JMT_GEMM_PPSPLIT_MIN_KT
+  if (min_kt < 0) {
+    const char* e = getenv("JMT_GEMM_PPSPLIT_MIN_KT");
+    min_kt = e ? atoi(e) : 27;
   }
-  if (tiles * 2 > ncu || tiles < min_tiles) return 0;
+  if (tiles * 2 > ncu || (long)(K / 64) * tiles < (long)min_kt * ncu) return 0;
   long s = ncu / tiles;
   const long smax = (K / 64) / 4;
   if (s > smax) s = smax;

@@ -20,7 +20,8 @@ struct GemmParams {
   float* ws;
   int64_t lda, ldb, ldc, ldaux;
   int64_t sA0, sA1, sB0, sB1, sC0, sC1;
-  int a_mode, b_mode, c_mode;   // 0 strided, 1 pointer per b0, 2 K-concat (a/b only)
+  int a_mode, b_mode, c_mode;   // 0 strided, 1 pointer per b0, 2 K-concat, 3 K-concat per b0
+                                // (a/b only; mode 3: sA0 / sB0 hold the segments per b0)
   int a_kseg, b_kseg;           // K-concat segment length (multiple of the K-tile)
   int M, N, K;
   int batch0, batch1;
@@ -113,10 +114,10 @@ template <typename T>
 __device__ __forceinline__ const T* operand_base(const void* const* ptrs, int mode, int64_t s0,
                                                  int64_t s1, int b0, int b1, int kseg, int k0,
                                                  int& kloc) {
-  if (mode == 2) {
-    const int seg = k0 / kseg;
+  if (mode >= 2) {               // K-concat: segment k0 / kseg (mode 3: of batch entry b0,
+    const int seg = k0 / kseg;   // s0 segments per entry)
     kloc = k0 - seg * kseg;
-    return (const T*)ptrs[seg];
+    return (const T*)ptrs[mode == 3 ? b0 * (int)s0 + seg : seg];
   }
   kloc = k0;
   const T* p = (const T*)ptrs[mode == 1 ? b0 : 0];

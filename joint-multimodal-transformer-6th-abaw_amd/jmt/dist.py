@@ -179,6 +179,19 @@ class GradBucketer:
                                          not self.world1):
             return
         if self.cuda:
+            from .graph import collective, segmented_capture_active
+            if segmented_capture_active():
+                # piecewise-captured step (jmt.graph.SegmentedStep): the bucket's all-reduce is
+                # issued on the host between two segment replays, ordered after the segment
+                # that wrote its gradients (the replay stream) and overlapping the next one
+                def issue(lo=lo, hi=hi):
+                    self.comm.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(self.comm):
+                        self.works.append(dist.all_reduce(self.flat[lo:hi],
+                                                          op=dist.ReduceOp.SUM,
+                                                          group=self.group, async_op=True))
+                collective(issue)
+                return
             # every stream that wrote one of the bucket's gradients (recorded by _done), the
             # stream this last notification came from, the weight-gradient side stream
             # (jmt.streams.run_side) and the step's compute stream precede the all-reduce; a
@@ -203,11 +216,18 @@ class GradBucketer:
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
-        for w in self.works:
-            w.wait()
+
+        def join():
+            for w in self.works:
+                w.wait()
+            if self.cuda:
+                torch.cuda.current_stream().wait_stream(self.comm)
+            self.works = []
         if self.cuda:
-            torch.cuda.current_stream().wait_stream(self.comm)
-        self.works = []
+            from .graph import collective
+            collective(join)              # deferred to replay under a SegmentedStep capture
+        else:
+            join()
 
     def close(self):
         for h in self._hooks:

@@ -917,7 +917,7 @@ def attn_backward(saved, go, dq, dk, dv):
         dS = torch.empty(N * H * Lq * ldp, dtype=cd, device=dev)
         pds = ops._attn_pds["on"] and _small_aligned(dq, qcol, cd) and _small_aligned(
             k_src, kcol, cd) and ops.attn_pds_ok(
-            Lq, Lk, dq.stride(0), sk_l, H)
+            Lq, Lk, dq.stride(0), max(sk_l, sv_l), H)
         dq_args = (_ptr(dq, qcol), (dq.stride(0), dq.stride(1)))
         ops.attn_bwd(_dc(cd), N, H, Lq, Lk, dh, go.data_ptr(), (so_l, so_n),
                      o.data_ptr(), (o.stride(0), o.stride(1)),
@@ -1093,8 +1093,11 @@ class CCCLossFn(Function):
             import torch.distributed as dist
             world = dist.get_world_size(group)
             if world > 1:
+                from .graph import collective
                 stats_all = torch.empty(8 * world, dtype=torch.float64, device=dev)
-                dist.all_gather_into_tensor(stats_all, stats, group=group)
+                # on the host between two segment replays under a SegmentedStep capture
+                collective(lambda sa=stats_all, st=stats:
+                           dist.all_gather_into_tensor(sa, st, group=group))
         loss = torch.empty((), dtype=torch.float32, device=dev)
         coef = torch.empty(8, dtype=torch.float64, device=dev)
         if add is not None and (add.dtype != torch.float32 or add.numel() != 1):

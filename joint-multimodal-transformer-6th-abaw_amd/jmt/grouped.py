@@ -116,6 +116,50 @@ def _gemm_wgrad(dy_ptrs: Sequence[int], ldy: int, sdy: int, x_ptrs: Sequence[int
     return dbt is not None
 
 
+def _kcat_ok(rows: int, n_ptrs: int, cd) -> bool:
+    """Whether a per-batch K-concatenated wgrad (jmt_gemm operand mode 3) applies: the segment
+    length (rows) a multiple of the 128-B K-tile and the pointer table within 8 entries."""
+    return (_merge_wgrads["on"] and cd != torch.float32 and rows % 64 == 0 and n_ptrs <= 8)
+
+
+# one weight-gradient launch for the two uses of each cross-attention module (K-concatenated
+# pairs) and for the encoders' W1 / W2 (JMT_WGRAD_MERGE=0: the round-5 launches, A/B switch)
+_merge_wgrads = {"on": os.environ.get("JMT_WGRAD_MERGE", "1") != "0"}
+
+
+def _gemm_wgrad_kcat(dy_segs, ldy: int, x_segs, ldx: int, rows: int, n: int, Ws, r0: int, cd,
+                     dev, bs=None) -> bool:
+    """W_g.grad[r0:r0+n] += sum_s dY[g][s]^T X[g][s]: each weight's uses as the K-segments of ONE
+    batch entry (jmt_gemm operand mode 3, K = len(segments) x rows), so the two uses of a module
+    are one (256 x 256 tile, K = 2 rows) item set of the split-K ping-pong kernel instead of two
+    12-tile launches on the 128 x 128 split plan.  With `bs`, b_g.grad += the column sums of all
+    of dY[g]'s segments (the row sums of A over the whole K).  Returns as _gemm_wgrad."""
+    from .functional import fused_bgrad_ok
+    nseg = len(dy_segs[0])
+    assert all(len(d) == nseg for d in dy_segs) and all(len(x) == nseg for x in x_segs)
+    grads = []
+    for W in Ws:
+        g = _grad_buffer(W)
+        grads.append(g if g is not None else torch.zeros_like(W))
+    dbt = None
+    if bs is not None and n > 1 and fused_bgrad_ok(cd):
+        dbt = []
+        for b in bs:
+            gb = _grad_buffer(b)
+            dbt.append(gb[r0:r0 + n] if gb is not None else
+                       torch.empty(n, dtype=torch.float32, device=dev))
+    Kin = Ws[0].shape[1]
+    ops.gemm(M=n, N=Kin, K=nseg * rows, ab_dtype=_dc(cd), c_dtype=ops.F32,
+             a=[p for d in dy_segs for p in d], lda=ldy, a_kmajor=False, a_mode=3, a_kseg=rows,
+             b=[p for x in x_segs for p in x], ldb=ldx, b_kmajor=False, b_mode=3, b_kseg=rows,
+             c=[_ptr(g, r0 * Kin) for g in grads], ldc=Kin, c_mode=1, batch0=len(Ws),
+             beta=1.0, dbias_tab=dbt, device=dev)
+    _grad_done(*Ws)
+    if dbt is not None:
+        _grad_done(*bs)
+    return dbt is not None
+
+
 def _bias_grad(dy2: torch.Tensor, ld: int, rows: int, n: int, b, r0: int):
     gb = _grad_buffer(b)
     if gb is not None:
@@ -464,9 +508,29 @@ class EncoderGroupFn(Function):
                     R * hid, cdt, cd, dev, aux=F1, ldaux=hid)
         # (W2's weight gradient stays on the compute stream: on the side stream the in-place
         # dH1 below would have to wait for it, which measured slower, profiles/r02_side_stream.txt)
-        b2_done = _gemm_wgrad([dS.data_ptr()], E, R * E, [F1.data_ptr()], hid, R * hid, R, E,
-                              [p[6] for p in P], 0, cd, dev,
-                              bs=None if b2_done else [p[7] for p in P]) or b2_done
+        # With hid == E, W1's weight gradient (dF1 and H1 are ready here) goes in the same launch:
+        # 2 G entries of 512 x 512 over the B T rows (24 tiles at G = 3: the split-K ping-pong
+        # kernel) instead of two 12-tile launches on the 128 x 128 split plan
+        merged = _merge_wgrads["on"] and hid == E and 2 * G <= 8 and cd != torch.float32
+        if merged:
+            ws = [p[6] for p in P] + [p[4] for p in P]
+            bsw = ([] if b2_done else [p[7] for p in P]) + [p[5] for p in P]
+            fused = _gemm_wgrad([dS[g].data_ptr() for g in range(G)] +
+                                [dF1[g].data_ptr() for g in range(G)], E, 0,
+                                [F1[g].data_ptr() for g in range(G)] +
+                                [H1[g].data_ptr() for g in range(G)], E, 0, R, E, ws, 0, cd, dev,
+                                bs=None if b2_done else bsw)
+            if not fused:
+                if not b2_done:
+                    _bias_grad_grouped(dS.data_ptr(), G, E, R * E, R, E, [p[7] for p in P], 0,
+                                       cd, dev)
+                _bias_grad_grouped(dF1.data_ptr(), G, hid, R * hid, R, hid, [p[5] for p in P], 0,
+                                   cd, dev)
+            b2_done = True
+        else:
+            b2_done = _gemm_wgrad([dS.data_ptr()], E, R * E, [F1.data_ptr()], hid, R * hid, R, E,
+                                  [p[6] for p in P], 0, cd, dev,
+                                  bs=None if b2_done else [p[7] for p in P]) or b2_done
         if not b2_done:
             _bias_grad_grouped(dS.data_ptr(), G, E, R * E, R, E, [p[7] for p in P], 0, cd, dev)
         # dH1 = dS2 + dF1 . W1  (in place on dS: beta = 1)
@@ -479,7 +543,8 @@ class EncoderGroupFn(Function):
                 _bias_grad_grouped(dF1.data_ptr(), G, hid, R * hid, R, hid, [p[5] for p in P], 0,
                                    cd, dev)
 
-        streams.run_side(w1_grads, reads=(dF1, H1))
+        if not merged:
+            streams.run_side(w1_grads, reads=(dF1, H1))
         # LN1: dS1 = d(X + A1)
         dS1 = torch.empty_like(dS)
         bo_done = ln_bwd(X, A1, dS, st1, [p[8] for p in P], [p[9] for p in P], dS1,
@@ -601,7 +666,25 @@ class CrossAttention6Fn(Function):
         _gemm_dgrad(dO6.data_ptr(), E, R * E, R, E, [M[m][2] for m, _, _ in pairs], 0,
                     dO.data_ptr(), E, R * E, cdt, cd, dev)
 
+        # the two uses of each module (one per half) as the K-segments of one batch entry
+        kcat = (len(halves) == 2 and len(halves[0]) == len(halves[1]) and
+                [pairs[i][0] for i in halves[0]] == [pairs[i][0] for i in halves[1]] and
+                _kcat_ok(R, 2 * len(halves[0]), cd))
+
         def out_proj_grads():
+            if kcat:
+                h0, h1 = halves
+                ms = [pairs[i][0] for i in h0]
+                if _gemm_wgrad_kcat([[_ptr(dO6, i * R * E), _ptr(dO6, j * R * E)]
+                                     for i, j in zip(h0, h1)], E,
+                                    [[O[i * B].data_ptr(), O[j * B].data_ptr()]
+                                     for i, j in zip(h0, h1)], E, R, E, [M[m][2] for m in ms],
+                                    0, cd, dev, bs=[M[m][3] for m in ms]):
+                    return
+                for m, i, j in zip(ms, h0, h1):
+                    _bias_grad(dO6[i], E, R, E, M[m][3], 0)
+                    _bias_grad(dO6[j], E, R, E, M[m][3], 0)
+                return
             rest = []
             for h in halves:
                 if not _gemm_wgrad([_ptr(dO6, i * R * E) for i in h], E, 0,
@@ -626,6 +709,26 @@ class CrossAttention6Fn(Function):
         # in_proj weight gradients (side stream, overlapping the stream dgrads): query rows
         # [0, E) from the query stream, key/value rows [E, 3E) from the key stream
         def in_proj_grads():
+            if kcat:
+                h0, h1 = halves
+                ms = [pairs[i][0] for i in h0]
+                ws = [M[m][0] for m in ms]
+                bs = [M[m][1] for m in ms]
+                seg = lambda off: [[_ptr(dQKV, i * R * 3 * E + off), _ptr(dQKV, j * R * 3 * E + off)]
+                                   for i, j in zip(h0, h1)]
+                fq = _gemm_wgrad_kcat(seg(0), 3 * E,
+                                      [[Y[pairs[i][1]].data_ptr(), Y[pairs[j][1]].data_ptr()]
+                                       for i, j in zip(h0, h1)], E, R, E, ws, 0, cd, dev, bs=bs)
+                fkv = _gemm_wgrad_kcat(seg(E), 3 * E,
+                                       [[Y[pairs[i][2]].data_ptr(), Y[pairs[j][2]].data_ptr()]
+                                        for i, j in zip(h0, h1)], E, R, 2 * E, ws, E, cd, dev,
+                                       bs=bs if fq else None)
+                if not (fq and fkv):
+                    assert not fq, "query-row bias sums fused without the key / value rows"
+                    for m, i, j in zip(ms, h0, h1):
+                        _bias_grad(dQKV[i], 3 * E, R, 3 * E, M[m][1], 0)
+                        _bias_grad(dQKV[j], 3 * E, R, 3 * E, M[m][1], 0)
+                return
             rest = []
             for h in halves:
                 ws = [M[pairs[i][0]][0] for i in h]

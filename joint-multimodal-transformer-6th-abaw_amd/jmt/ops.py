@@ -291,7 +291,7 @@ def attn_pds_ok(Lq, Lk, sdq_l, sk_l, H) -> bool:
     128-row dQ tile and Lk K rows within 32-bit byte offsets."""
     ldp = attn_dkdv_ldp(Lk)
     lim = 1 << 31
-    return ((Lq + 128) * ldp * 2 < lim and sdq_l >= H * 512 and 128 * sdq_l * 2 < lim
+    return ((Lq + 128) * ldp * 2 < lim // 2 and sdq_l >= H * 512 and 128 * sdq_l * 2 < lim
             and Lk * sk_l * 2 < lim)
 
 

@@ -153,7 +153,7 @@ def test_bench_gpus2_gloo_on_one_gpu():
     assert len(lines) == 1
     j = json.loads(lines[0])
     assert j["n_gpus"] == 2 and j["launcher"] == "bench.py" and j["dist_backend"] == "gloo"
-    assert j["graph"] is False                               # N > 1 default: eager step
+    assert j["graph"] is True and "segments" in j["graph_kind"]   # N > 1: segmented graph
     assert j["config"]["global_batch"] == 8
     assert j["parity"]["pass"], j["parity"]
     assert "[rank 0] rank 0/2" in r.stderr and "[rank 1] rank 1/2" in r.stderr

@@ -1119,7 +1119,7 @@ def test_layernorm_grouped_equals_per_group(dsum, cd):
             assert close(a[3][i], b[3][i])
 
 
-@pytest.mark.parametrize("ak,bk", [(False, False), (True, True), (True, False)])
+@pytest.mark.parametrize("ak,bk", [(False, False), (True, True), (True, False), (False, True)])
 def test_gemm_pp_split_k(ak, bk):
     """Split-K ping-pong kernel (cfg 44, gemm_persist.hip gemm_pp_split_kernel): items are
     (256 x 256 tile, split) with balanced K-tile ranges, fp32 partial slabs reduced by
@@ -1165,6 +1165,77 @@ def test_gemm_pp_split_k(ak, bk):
                         assert rerr <= 1e-6 * Al[i].abs().sum(1).max().item() + 1e-5, (M, K, rerr)
         if not ak and not bk:
             assert torch.equal(outs[0], outs[1]), "row sums changed C"
+
+
+@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("ak,bk", [(False, False), (False, True)])
+def test_gemm_kconcat_split_k(mode, ak, bk):
+    """K-concatenated operands on the split-K kernels: mode 2 (segments shared by
+    every batch entry) and mode 3 (ABI 7: each batch entry's own segments, base[b0 * nseg + s] —
+    the two uses of a cross-attention module in one weight-gradient entry).  The split ranges
+    start partway through a segment (K-tiles per split not dividing the segment); cfg 44 (split-K
+    ping-pong, the planner's choice for the merged wgrads), cfg 5 and the planner's default vs
+    the fp32 sum of the per-segment products, with beta = 1 and (TN) the A row sums over all
+    segments."""
+    from jmt import _lib
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(45)
+    cases = [(512, 512, 19200, 2, 3, None), (512, 256, 1344, 2, 2, 7), (256, 512, 2240, 3, 2, 5)]
+    for (M, N, kseg, nseg, nb, splits) in cases:
+        if mode == 2 and nb > 1 and splits is None:
+            nb = 1
+        A, B = [], []
+        for i in range(nb if mode == 3 else 1):
+            for _ in range(nseg):
+                A.append(_operand(M, kseg, ak, BF16, gen=g))
+                B.append(_operand(N, kseg, bk, BF16, gen=g))
+        lda, ldb = A[0][2], B[0][2]
+        C0 = torch.randn(nb, M, N, device=DEV, generator=g)
+        refs, rrefs = [], []
+        for i in range(nb):
+            ss = range(i * nseg, (i + 1) * nseg) if mode == 3 else range(nseg)
+            refs.append(C0[i] + sum(A[s][1][0] @ B[s][1][0].transpose(0, 1) for s in ss))
+            rrefs.append(sum(A[s][1][0].sum(1) for s in ss))
+        if splits is None:
+            assert ops.auto_splits(M, N, nseg * kseg, nb, BF16) >= 2
+        for cfg in (44, 5, 0):
+            rs = not ak and not bk
+            C = C0.clone()
+            db = [torch.zeros(M, device=DEV) for _ in range(nb)] if rs else None
+            lib.jmt_gemm_set_debug(cfg << 8)
+            try:
+                ops.gemm(M=M, N=N, K=nseg * kseg, ab_dtype=BF16, c_dtype=F32,
+                         a=[t[0].data_ptr() for t in A], lda=lda, a_kmajor=ak, a_mode=mode,
+                         a_kseg=kseg, b=[t[0].data_ptr() for t in B], ldb=ldb, b_kmajor=bk,
+                         b_mode=mode, b_kseg=kseg, c=[C[i].data_ptr() for i in range(nb)],
+                         ldc=N, c_mode=1, batch0=nb, beta=1.0, splits=splits, dbias_tab=db,
+                         device=DEV)
+            finally:
+                lib.jmt_gemm_set_debug(0)
+            torch.cuda.synchronize()
+            for i in range(nb):
+                scale = sum((A[s][1][0].abs() @ B[s][1][0].abs().transpose(0, 1)).max().item()
+                            for s in range(nseg))
+                err = (C[i] - refs[i]).abs().max().item()
+                assert err <= 2e-3 * scale, (mode, M, N, kseg, cfg, i, err)
+                if rs:
+                    rerr = (db[i] - rrefs[i]).abs().max().item()
+                    assert rerr <= 1e-5 * nseg * kseg, (mode, cfg, i, rerr)
+
+
+def test_gemm_kconcat_per_batch_rejects_short_table():
+    """Mode 3 needs batch0 x ceil(K / kseg) pointers and a kseg of whole K-tiles."""
+    from jmt import _lib
+    x = torch.zeros(64, 64, device=DEV, dtype=torch.bfloat16)
+    c = torch.zeros(2, 64, 64, device=DEV)
+    for kseg, na in ((64, 3), (48, 4)):
+        with pytest.raises(RuntimeError, match="per-batch K-concat"):
+            ops.gemm(M=64, N=64, K=128, ab_dtype=BF16, c_dtype=F32, a=[x.data_ptr()] * na,
+                     lda=64, a_kmajor=False, a_mode=3, a_kseg=kseg, b=[x.data_ptr()] * 4,
+                     ldb=64, b_kmajor=False, b_mode=3, b_kseg=64,
+                     c=[c[0].data_ptr(), c[1].data_ptr()], ldc=64, c_mode=1, batch0=2,
+                     device=DEV)
+    assert _lib.load() is not None
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 5, 10, 11, 20, 21])
