@@ -697,19 +697,20 @@ def main():
     # all-gather, per-bucket RCCL all-reduces, the final join) issued eagerly between them
     # (jmt.graph.SegmentedStep): host issue is one graph launch per segment instead of the
     # eager step's ~300 launches (host_issue_ms_per_eager_step, ~3 ms at c3), which a
-    # strong-scaling B = 8 per GPU step would not hide.  JMT_GRAPH_DIST=0: eager;
-    # JMT_GRAPH_DIST=1: the RCCL collectives captured into one whole-step graph
-    # (tests/test_gpu_dist.py test_rccl_bucketed_step_sync_free_and_capturable, world size 1).
+    # strong-scaling B = 8 per GPU step would not hide.  JMT_GRAPH_DIST=0: eager.  (Round 5's
+    # JMT_GRAPH_DIST=1 — RCCL captured into one whole-step graph — is retired: ProcessGroupNCCL's
+    # watchdog intermittently aborted a rank on a work event recorded inside the capture.)
     gmode = os.environ.get("JMT_GRAPH_DIST", "segmented")
-    use_graph = args.graph and (world == 1 or gmode in ("1", "segmented"))
+    use_graph = args.graph and (world == 1 or gmode != "0")
     graph_kind = None
     if use_graph:
-        if world == 1 or gmode == "1":
+        if world == 1:
             # the whole step as one hipGraph (jmt/graph.py): replay issues ~300 launches at once
             graphed = GraphedStep(step).capture(warmup=1)
             graph_kind = "whole step"
         else:
             from jmt.graph import SegmentedStep
+            loss = None         # no eager step's autograd graph may outlive into the capture
             graphed = SegmentedStep(step).capture(warmup=1)
             graph_kind = f"{len(graphed.segments)} segments, collectives eager between them"
         run = graphed.replay

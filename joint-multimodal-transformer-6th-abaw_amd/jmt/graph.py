@@ -87,7 +87,9 @@ class SegmentedStep:
     next segment; replay() runs segment, collective, segment, ... in capture order on the
     current stream, so each bucket's all-reduce still overlaps the rest of the backward.
     Requirements as GraphedStep, plus: no forked stream may be open across a collective (the
-    weight-gradient side stream is turned off while capturing)."""
+    weight-gradient side stream is turned off while capturing), and the caller holds no output
+    of an earlier eager step (its autograd graph would keep the parameters' AccumulateGrad nodes,
+    created on another stream, so their hooks — the bucket notifications — run on that stream)."""
 
     def __init__(self, step_fn: Callable[[], object]):
         self.step_fn = step_fn
@@ -140,10 +142,13 @@ class SegmentedStep:
         self._g = None
 
     def cut(self, op: Callable[[], object]):
-        cur = torch.cuda.current_stream()
-        if cur != self._stream:
-            raise RuntimeError("SegmentedStep: a collective was reached on a forked stream "
-                               "(a segment cannot end with unjoined work)")
+        if torch.cuda.current_stream() != self._stream:
+            # e.g. the post-accumulate hook of a parameter whose AccumulateGrad node was created
+            # on another stream by an eager step whose outputs the caller still holds (their
+            # autograd graph keeps the node alive): drop those outputs before capture()
+            raise RuntimeError("SegmentedStep: a collective was reached on a forked stream (a "
+                               "segment cannot end with unjoined work); release the outputs of "
+                               "earlier eager steps before capture()")
         self._end(op)
         self._begin()
 

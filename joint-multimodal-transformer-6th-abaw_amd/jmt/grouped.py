@@ -666,15 +666,19 @@ class CrossAttention6Fn(Function):
         _gemm_dgrad(dO6.data_ptr(), E, R * E, R, E, [M[m][2] for m, _, _ in pairs], 0,
                     dO.data_ptr(), E, R * E, cdt, cd, dev)
 
-        # the two uses of each module (one per half) as the K-segments of one batch entry
+        # the two uses of each module (one per half) as the K-segments of one batch entry:
+        # h0[u] and h1[u] are the pairs of module ms[u]
         kcat = (len(halves) == 2 and len(halves[0]) == len(halves[1]) and
-                [pairs[i][0] for i in halves[0]] == [pairs[i][0] for i in halves[1]] and
+                sorted(pairs[i][0] for i in halves[0]) ==
+                sorted(pairs[i][0] for i in halves[1]) and
                 _kcat_ok(R, 2 * len(halves[0]), cd))
+        if kcat:
+            h0 = list(halves[0])
+            ms = [pairs[i][0] for i in h0]
+            h1 = [next(j for j in halves[1] if pairs[j][0] == m) for m in ms]
 
         def out_proj_grads():
             if kcat:
-                h0, h1 = halves
-                ms = [pairs[i][0] for i in h0]
                 if _gemm_wgrad_kcat([[_ptr(dO6, i * R * E), _ptr(dO6, j * R * E)]
                                      for i, j in zip(h0, h1)], E,
                                     [[O[i * B].data_ptr(), O[j * B].data_ptr()]
@@ -710,8 +714,6 @@ class CrossAttention6Fn(Function):
         # [0, E) from the query stream, key/value rows [E, 3E) from the key stream
         def in_proj_grads():
             if kcat:
-                h0, h1 = halves
-                ms = [pairs[i][0] for i in h0]
                 ws = [M[m][0] for m in ms]
                 bs = [M[m][1] for m in ms]
                 seg = lambda off: [[_ptr(dQKV, i * R * 3 * E + off), _ptr(dQKV, j * R * 3 * E + off)]

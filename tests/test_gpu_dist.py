@@ -404,11 +404,13 @@ def _rccl1_worker(rank, world, port, q, mode):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["sync", "graph"])
+@pytest.mark.parametrize("mode", ["sync"])
 def test_rccl_bucketed_step_sync_free_and_capturable(mode):
-    """a bucketed step issues no device synchronisation, and the N>1 step
-    (RCCL all-reduces on the communication stream, gated per bucket) captures into a hipGraph
-    whose replay matches eager steps exactly."""
+    """a bucketed step issues no device synchronisation.  (Its 'graph' mode —
+    the RCCL all-reduces captured into one whole-step hipGraph — is retired with that path in
+    round 6: ProcessGroupNCCL's watchdog thread intermittently queried a work event recorded
+    inside the capture and aborted the rank, hipErrorCapturedEvent; the N>1 step is now the
+    segmented graph with eager collectives, test_segmented_graph_step_matches_eager.)"""
     out = _spawn(_rccl1_worker, (mode,), world=1)
     (_, nb, launched, same), = out
     assert nb > 2 and launched == nb, (nb, launched)
