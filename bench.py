@@ -36,7 +36,7 @@ for _p in (REPO, PKG):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-PROFILE_TAG = "r05"            # profiles/<tag>_pmc_bench/ (PMC traffic), <tag>_family_trace.json
+PROFILE_TAG = "r06"            # profiles/<tag>_pmc_bench/ (PMC traffic), <tag>_family_trace.json
 PEAK_BF16_TFLOPS = 2516.6      # 256 CU x 4 SIMD x 1024 flop/clk (16x16x32 bf16 / 16 cyc) x 2.4 GHz
 PEAK_HBM_GBS = 8000.0
 D_A, D_V, E = 1024, 2048, 512
@@ -206,7 +206,11 @@ class FamilyProbe:
                         "gflop_per_launch": round(d["flops"] / d["launches"] / 1e9, 3),
                         "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
                         "tflops": round(tf, 1), "frac": round(tf / PEAK_BF16_TFLOPS, 4)})
-            if f.startswith(("small_attn", "attn_short")):   # HBM-bound families: bytes
+            if f.startswith(("small_attn", "attn_short", "attn_bwd", "attn_dkdv")):
+                # HBM-bound families: algorithmic bytes per launch (jmt.ops hooks).  The attention
+                # backward pair at dh = 512 moves ~92 FLOP per byte (Q, dO, O, K, V read, P / dS
+                # handed over) against a machine balance of ~400: its roofline is HBM, the MFMA
+                # fraction beside it is the secondary view
                 gbs = d["bytes"] / (d["ms"] * 1e-3) / 1e9
                 out[-1].update({"bound": "hbm", "gbps": round(gbs, 1),
                                 "hbm_frac": round(gbs / PEAK_HBM_GBS, 4)})

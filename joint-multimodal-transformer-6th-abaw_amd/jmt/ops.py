@@ -274,9 +274,10 @@ def attn_bwd(dtype, N, H, Lq, Lk, dh, go_ptr, sgo, o_ptr, so, q_ptr, sq, k_ptr, 
     # bytes: dO, O, Q, K, V, (dQ,) lse and the P / dS rows handed to attn_dkdv
     es = 4 if dtype == F32 else 2
     nrow = 3 if dq_ptr is None else 4
+    lw = -(-Lk // 32) * 32 if dq_ptr is None else ldp     # P / dS columns written
     _hooked({"family": "attn_bwd", "flops": 4.0 * N * H * Lq * Lk * dh,
              "bytes": float(N * H) * ((nrow * Lq + 2 * Lk) * dh * es + 4 * Lq +
-                                      2 * Lq * ldp * es)}, launch)
+                                      2 * Lq * lw * es)}, launch)
 
 
 _attn_dkdv = {"on": os.environ.get("JMT_ATTN_DKDV", "1") != "0"}

@@ -59,7 +59,7 @@ def family(name: str):
         return "attn_short_bwd"
     if "attn_fwd_kernel" in name:
         return "attn_fwd"
-    if "attn_bwd_kernel" in name:
+    if "attn_bwd_kernel" in name or "attn_bwd_pds_kernel" in name:
         return "attn_bwd"
     if "attn_dkdv_kernel" in name:
         return "attn_dkdv"

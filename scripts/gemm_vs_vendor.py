@@ -39,6 +39,11 @@ SHAPES = [
     ("TN b3 512x512x19200", "TN", 3, 512, 512, R),
     ("TN b3 1536x512x19200", "TN", 3, 1536, 512, R),
     ("TN b6 1024x512x19200", "TN", 6, 1024, 512, R),
+    # round 6: the merged weight gradients (encoder W1 + W2 as b6; a cross-attention module's
+    # two uses as one K = 2 B T entry, timed here as a plain long-K TN)
+    ("TN b6 512x512x19200", "TN", 6, 512, 512, R),
+    ("TN b3 512x512x38400", "TN", 3, 512, 512, 2 * R),
+    ("TN b3 1024x512x38400", "TN", 3, 1024, 512, 2 * R),
 ]
 
 
