@@ -1184,7 +1184,11 @@ def check_ce_labels(dev=None, extra=None):
 class CELossFn(Function):
     """losses/loss.py:34-51 CELoss on the device: digitize + weighted log-softmax NLL in one
     statistics kernel, (optional) all-gather of 4 doubles per rank, one finish kernel; backward
-    one elementwise kernel.  No host synchronisation (the reference digitizes on the host)."""
+    one elementwise kernel.  Host synchronisation: one read of the out-of-range label count per
+    eager call (`CE_EAGER_LABEL_CHECK`, default on: the reference's own digitize reads the labels
+    on the host at the same point, loss.py:48, and F.cross_entropy raises there); with it off, and
+    always under graph capture, the count accumulates on the device and `check_ce_labels()` raises
+    on it later, so the step issues without a host read."""
 
     @staticmethod
     def forward(ctx, x, label, k, lo, hi, weights, group):
@@ -1220,8 +1224,11 @@ class CELossFn(Function):
             import torch.distributed as dist
             world = dist.get_world_size(group)
             if world > 1:
+                from .graph import collective
                 stats_all = torch.empty(4 * world, dtype=torch.float64, device=dev)
-                dist.all_gather_into_tensor(stats_all, stats, group=group)
+                # deferred to between two segment replays under a SegmentedStep capture
+                collective(lambda sa=stats_all, st=stats:
+                           dist.all_gather_into_tensor(sa, st, group=group))
         loss = torch.empty((), dtype=torch.float32, device=dev)
         coef = torch.empty(1, dtype=torch.float64, device=dev)
         ops.ce_finish(world, stats_all, loss, coef)
