@@ -1260,8 +1260,17 @@ int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int 
   // step shape by 9-20 % (profiles/r04/gemm_persist_vs_vendor_a.jsonl); cfg 43 beats cfg 40 by
   // 14-25 % on the same shapes (profiles/r05/step_ab_persist40_vs_pp43.txt), and cfg 45 (32-MFMA phases) beats cfg 43 in the step: 4.266 ->
   // 4.193 ms, NT 0.91 -> 0.87, NN 0.87 -> 0.81 ms/step (profiles/r05/step_ab_pp43_vs_pp45.txt)
+  // Round 6: cfg 45 also wins below that on the single-batch B*T-row shapes the gate used to
+  // leave on the 160x256 tile (NT 19200x512x2048 53.5 -> 47.8 us with 150 tiles, NT x1024x3072
+  // 144 -> 138, NN x512x3072 83 -> 71, NN x1024x256 32 -> 28; profiles/r06/b1_cfg_sweep.jsonl):
+  // the gate is now half a tile per CU (JMT_GEMM_PP_MINW2 = 2 W / CUs threshold, 3 before).
+  static int minw2 = -1;
+  if (minw2 < 0) {
+    const char* e = getenv("JMT_GEMM_PP_MINW2");
+    minw2 = e ? atoi(e) : 1;
+  }
   const long W = (long)(d->M / 256) * (d->N / 256) * batch0 * (d->batch1 < 1 ? 1 : d->batch1);
-  return W * 2 >= 3L * num_cus() ? 45 : 0;
+  return W * 2 >= (long)minw2 * num_cus() ? 45 : 0;
 }
 
 }  // namespace jmt

@@ -33,6 +33,7 @@ SHAPES = [
     ("NN b1 19200x512x3072", "NN", 1, R, 512, 3072),
     ("NN b1 19200x1024x256", "NN", 1, R, 1024, 256),
     ("NT b2 19200x128x1024", "NT", 2, R, 128, 1024),
+    ("NN b2 19200x512x512", "NN", 2, R, 512, 512),      # out_layer_pv's stacked-stream dgrad
     ("NN b3 19200x512x512", "NN", 3, R, 512, 512),
     ("NN b6 19200x512x1024", "NN", 6, R, 512, 1024),
     ("NN b3 19200x512x1536", "NN", 3, R, 512, 1536),
