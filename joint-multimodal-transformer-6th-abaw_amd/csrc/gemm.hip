@@ -821,7 +821,7 @@ extern "C" int jmt_gemm(const jmt_gemm_desc* d, void* stream) {
   {
     const int pc = persist_choice(d, p, splits, cfg);
     if (pc) {
-      p.tiles_m = d->M / 256;
+      p.tiles_m = (d->M + 255) / 256;                 // cfg 45: the last row panel may be partial
       p.tiles_n = d->N / 256;
       const int W = p.tiles_m * p.tiles_n * batch0 * batch1;
       const int ncu = num_cus_persist();

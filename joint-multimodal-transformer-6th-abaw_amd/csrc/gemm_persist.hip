@@ -131,11 +131,15 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 // head and it waited vmcnt(4) there, draining the next K-tile's DMA every iteration)
 // rows I0 .. I0 + NI - 1 of the wave's sub-tiles (the ping-pong kernel stores its two 64-row
 // halves in two segments)
+// part (cfg 45 only, M % 256 != 0): the item is the last row panel, rows >= M exist only in the
+// tile — the beta * C / mask loads read row M - 1 instead and the stores go through a buffer
+// resource that ends at row M, so the hardware drops them; the VMEM count stays the full tile's
+// (the deadline counts above depend on it).
 template <typename T, class C, int EPI, int I0 = 0, int NI = C::TM>
 __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PItem& it,
                                                  f32x4 (&acc)[C::TM][C::TN],
                                                  const float* bias_lds, int lane, int wm, int wn,
-                                                 bool nostore = false) {
+                                                 bool nostore = false, bool part = false) {
   static_assert(C::TN % 2 == 0, "paired stores");
   T* cp;
   int64_t cbase;
@@ -189,7 +193,8 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
   u32x2 cr[2][C::TN], ar[2][C::TN];
   constexpr bool ldc_ = (EPI & 1) != 0, lda_ = (EPI & 2) != 0;
   auto load_row = [&](int i, u32x2 (&c)[C::TN], u32x2 (&a)[C::TN]) {
-    const int m = it.m0 + wm * C::WTM + 16 * i + rl;
+    int m = it.m0 + wm * C::WTM + 16 * i + rl;
+    if (part) m = min(m, p.M - 1);
 #pragma unroll
     for (int j = 0; j < C::TN; ++j) {
       const int n = it.n0 + wn * C::WTN + 16 * j + 4 * g;
@@ -238,6 +243,22 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
       vj[jp] = u32x4{r0[0], r1[0], r0[1], r1[1]};
     }
     if (nostore) continue;
+    if (part) {
+      // byte offsets from the entry's C base; rows >= M lie past num_records
+      const uint64_t ba = (uint64_t)(uintptr_t)(cp + cbase);
+      const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)ba);
+      const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(ba >> 32));
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(((uint64_t)bhi << 32) | blo), 0, (int)((int64_t)p.M * p.ldc * (int64_t)sizeof(T)),
+          0x00020000);
+      const int row = it.m0 + wm * C::WTM + 16 * i + rl;
+      const int col = it.n0 + wn * C::WTN + 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll
+      for (int jp = 0; jp < C::TN / 2; ++jp)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            vj[jp], rsrc, (int)(((int64_t)row * p.ldc + col + 32 * jp) * (int64_t)sizeof(T)), 0, 0);
+      continue;
+    }
     T* const crow = cl + (int64_t)(16 * i) * p.ldc;
 #pragma unroll
     for (int jp = 0; jp < C::TN / 2; ++jp) {
@@ -826,15 +847,14 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
   const int64_t ld = ISA ? p.lda : p.ldb;
   // per-lane byte offsets of this wave's instructions 2 wl, 2 wl + 1 of each half (h) of its
   // operand's k-half image, relative to the operand's K-tile base
-  int64_t off[2][2];
+  // (the A rows of a last, partial row panel (M % 256 != 0) are clamped to the last row — or the
+  // last 8-row chunk, MN-major — in set_stream; their products are never stored)
+  int rowv[2][2], kkv[2][2];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      int row, kk;
-      chunk_src<T, KM, 64, 256>((8 * h + 2 * wl + e) * 64 + lane, row, kk);
-      off[h][e] = (KM ? (int64_t)row * ld + kk : (int64_t)kk * ld + row) * (int64_t)sizeof(T);
-    }
+    for (int e = 0; e < 2; ++e)
+      chunk_src<T, KM, 64, 256>((8 * h + 2 * wl + e) * 64 + lane, rowv[h][e], kkv[h][e]);
   const int64_t dk = (KM ? (int64_t)64 : (int64_t)64 * ld) * (int64_t)sizeof(T);   // K-tile
   const int64_t hk = dk / 2;                                                          // k-half
   const int seg = (ISA ? p.a_mode : p.b_mode) >= 2 ? (ISA ? p.a_kseg : p.b_kseg) / 64 : 1 << 30;
@@ -852,10 +872,15 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
                                        p.b_kseg, k0, kl);
     const int r0 = ISA ? iss_it.m0 : iss_it.n0;
     const char* sx = (const char*)(KM ? X + (int64_t)r0 * ld + kl : X + (int64_t)kl * ld + r0);
+    const int rmax = ISA ? p.M - (KM ? 1 : 8) - r0 : 256;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) ps[h][e] = sx + off[h][e];
+      for (int e = 0; e < 2; ++e) {
+        const int r = min(rowv[h][e], rmax);
+        ps[h][e] = sx + (KM ? (int64_t)r * ld + kkv[h][e] : (int64_t)kkv[h][e] * ld + r) *
+                            (int64_t)sizeof(T);
+      }
     left = seg - (kl >> 6);
   };
   auto next_ktile = [&]() {
@@ -943,7 +968,8 @@ __device__ __forceinline__ void pp2_run(const GemmParams& p, uint32_t lbase, con
         rsum[0] = rsum[1] = 0.f;
       }
     } else {
-      persist_epilogue<T, C, EPI>(p, cur, acc, bias_lds, lane, wm, wn);
+      persist_epilogue<T, C, EPI>(p, cur, acc, bias_lds, lane, wm, wn, false,
+                                  cur.m0 + 256 > p.M);
     }
   };
   for (int t = 0; t < nT; ++t) {
@@ -1237,6 +1263,16 @@ extern "C" int jmt_gemm_pp_stamps_read(uint64_t* host, int n) {
 
 namespace jmt {
 
+// JMT_GEMM_PP_MPART=0: partial row panels (M % 256 != 0) off the ping-pong kernel by default
+static int mpart_env() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("JMT_GEMM_PP_MPART");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
 int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int forced) {
   static int env = -1;
   if (env < 0) {
@@ -1247,13 +1283,20 @@ int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int 
   const int batch0 = d->batch0 < 1 ? 1 : d->batch0;
   const long nbias = p.bias_mode == 1 ? (long)(d->n_bias > 0 ? batch0 : 1) * d->N : 0;
   // (beta * C / the ReLU mask: 8-B loads of C / aux rows in the epilogue — c_vec4 covers aux)
+  // M % 256 != 0 (c2's 9,600 rows): cfg 45 only — its last row panel clamps the A rows and stores
+  // through a buffer resource ending at row M (32-bit byte offsets over the panel's rows)
+  const bool mfull = d->M % 256 == 0;
+  const int64_t mpad = (int64_t)(d->M + 256) * (int64_t)dtype_size(dt);
+  const bool mpart = !mfull && d->M % 8 == 0 && mpad * d->ldc < (1LL << 31) &&
+                     (d->aux == nullptr || mpad * d->ldaux < (1LL << 31));
   const bool ok = dt != JMT_F32 && d->c_dtype == dt && splits == 1 && d->n_dbias == 0 &&
-                  d->M % 256 == 0 && d->N % 256 == 0 && d->K % 64 == 0 && d->K >= 128 &&
+                  (mfull || mpart) && d->N % 256 == 0 && d->K % 64 == 0 && d->K >= 128 &&
                   p.c_vec8 && p.c_vec4 && p.bias_mode != 2 && nbias <= kPersistBias;
   if (!ok) return 0;
-  if (forced == 40 || forced == 43 || forced == 45) return forced;
+  if (forced == 45 || (mfull && (forced == 40 || forced == 43))) return forced;
   if (forced != 0 || env == 0) return 0;
-  if (env == 40 || env == 43 || env == 45) return env;
+  if (env == 45 || (mfull && (env == 40 || env == 43))) return env;
+  if (!mfull && !mpart_env()) return 0;
   // default: the ping-pong kernel (cfg 43) wherever the launch has at least 1.5 tiles per CU
   // (below that the 160x256 / split tiles of the one-block-per-tile kernel quantise better: NT
   // 19200x512x2048 53 vs 68 us).  cfg 40 beat the one-block-per-tile kernel on every batched
@@ -1269,7 +1312,8 @@ int persist_choice(const jmt_gemm_desc* d, const GemmParams& p, int splits, int 
     const char* e = getenv("JMT_GEMM_PP_MINW2");
     minw2 = e ? atoi(e) : 1;
   }
-  const long W = (long)(d->M / 256) * (d->N / 256) * batch0 * (d->batch1 < 1 ? 1 : d->batch1);
+  const long W = (long)((d->M + 255) / 256) * (d->N / 256) * batch0 *
+                 (d->batch1 < 1 ? 1 : d->batch1);
   return W * 2 >= (long)minw2 * num_cus() ? 45 : 0;
 }
 

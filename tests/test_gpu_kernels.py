@@ -195,6 +195,84 @@ def test_gemm_kconcat_and_pointer_tables(dt):
     assert (dW - ref).abs().max().item() <= _tol(dt, M) * ref.abs().max().item()
 
 
+def _kernel_names(fn):
+    """Names of the device kernels fn() launches (torch.profiler; None if it records none)."""
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+    return names or None
+
+
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_pp_partial_row_panel(ak, bk):
+    """cfg 45 (ping-pong persistent GEMM) with M % 256 != 0 (round 6: c2's 9,600 rows): the last
+    row panel's A rows are clamped and its stores go through a buffer resource ending at row M.
+    vs torch fp32 for the plain / bias-table + ReLU / beta * C / ReLU-mask epilogues, batched with
+    guard rows between the entries' C blocks that must stay untouched, dbg 32 bit-identical, and
+    the default plan takes the ping-pong kernel for such a shape (kernel name via torch.profiler)."""
+    from jmt import _lib
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(45)
+    bf = torch.bfloat16
+    GUARD = 40                           # rows of sentinel after each entry's M rows
+    for (M, N, K, nb) in [(9600, 512, 512, 2), (1000, 768, 256, 3), (264, 256, 128, 1)]:
+        A, Al, lda, sa = _operand(M, K, ak, BF16, batch=nb, gen=g)
+        Bs, Bl_t, ldb, sb = _operand(N, K, bk, BF16, batch=nb, gen=g)
+        Bl = Bl_t.transpose(1, 2)
+        bias = [torch.randn(N, device=DEV, generator=g) for _ in range(nb)]
+        C0 = torch.randn(nb, M + GUARD, N, device=DEV, generator=g).to(bf)
+        aux = torch.randn(nb, M + GUARD, N, device=DEV, generator=g).to(bf)
+        for form in ("bias_relu", "beta", "mask"):
+            kw = dict(M=M, N=N, K=K, ab_dtype=BF16, c_dtype=BF16, a=[A.data_ptr()], lda=lda,
+                      a_kmajor=ak, sA=(sa, 0), b=[Bs.data_ptr()], ldb=ldb, b_kmajor=bk,
+                      sB=(sb, 0), ldc=N, sC=((M + GUARD) * N, 0), batch0=nb, splits=1,
+                      device=DEV)
+            if form == "bias_relu":
+                kw.update(alpha=0.75, bias_tab=bias, bias_mode=1, relu=True)
+            elif form == "beta":
+                kw.update(beta=0.5)
+            else:
+                kw.update(aux=aux, ldaux=N)
+            outs = []
+            for dbg in (0, 32):
+                C = C0.clone()
+                lib.jmt_gemm_set_debug((45 << 8) | dbg)
+                try:
+                    ops.gemm(c=[C.data_ptr()], **kw)
+                finally:
+                    lib.jmt_gemm_set_debug(0)
+                outs.append(C)
+            assert torch.equal(outs[0], outs[1]), (M, form, "dbg 32 changed the result")
+            C = outs[0]
+            assert torch.equal(C[:, M:], C0[:, M:]), (M, form, "stores past row M")
+            for i in range(nb):
+                ref = Al[i] @ Bl[i]
+                if form == "bias_relu":
+                    ref = torch.relu(0.75 * ref + bias[i])
+                elif form == "beta":
+                    ref = ref + 0.5 * C0[i, :M].float()
+                else:
+                    ref = torch.where(aux[i, :M].float() > 0, ref, torch.zeros_like(ref))
+                err = (C[i, :M].float() - ref).abs().max().item()
+                assert err <= 1e-2 * ref.abs().max().item(), (M, N, K, form, i, err)
+    # the default plan: a 9,600-row launch of >= 128 tiles runs on the ping-pong kernel
+    M, N, K, nb = 9600, 512, 512, 2
+    A, Al, lda, sa = _operand(M, K, ak, BF16, batch=nb, gen=g)
+    Bs, Bl_t, ldb, sb = _operand(N, K, bk, BF16, batch=nb, gen=g)
+    Bl = Bl_t.transpose(1, 2)
+    C = torch.empty(nb, M, N, device=DEV, dtype=bf)
+    names = _kernel_names(lambda: ops.gemm(
+        M=M, N=N, K=K, ab_dtype=BF16, c_dtype=BF16, a=[A.data_ptr()], lda=lda, a_kmajor=ak,
+        sA=(sa, 0), b=[Bs.data_ptr()], ldb=ldb, b_kmajor=bk, sB=(sb, 0), c=[C.data_ptr()],
+        ldc=N, sC=(M * N, 0), batch0=nb, device=DEV))
+    if names is not None:
+        assert any("gemm_pp2_kernel" in n for n in names), names
+    ref = torch.bmm(Al, Bl.contiguous())
+    assert (C.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("cfg", [40, 43, 45])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 def test_gemm_persistent(cfg, ak, bk):
