@@ -272,6 +272,9 @@ __device__ __forceinline__ void persist_epilogue(const GemmParams& p, const PIte
 // split-K form of the epilogue (ping-pong kernel, p.splits > 1): rows I0 .. I0 + NI - 1 of the
 // wave's sub-tiles as raw fp32 partial sums into the item's slab, ws[(sp nb + b) M + m][n] (the
 // layout splitk_reduce_kernel sums in split order): one 16-B store per sub-tile and lane
+// (nontemporal; plain stores, which could leave the slabs in the last-level cache for the
+// reduce, measured the same in the step: 4.067-4.082 vs 4.066-4.075 ms, profiles/r06/
+// step_ab_slab_nt.txt)
 template <class C, int I0, int NI>
 __device__ __forceinline__ void pp_slab_epilogue(const GemmParams& p, const PItem& it,
                                                  const f32x4 (&acc)[C::TM][C::TN], int lane,

@@ -590,6 +590,8 @@ __device__ __forceinline__ void reduce_outputs(const GemmParams& p, int b, int m
   const float* src0 = p.ws + (int64_t)b * per + mn;
   int s = 0;
   if constexpr (W == 4) {
+    // (every slab load of up to 32 splits issued before the first add measured slower: 19.7 vs
+    // 17.3 us per reduce launch in the c3 step, profiles/r06/reduce_prof_all_loads_first.csv vs reduce_prof_rowsum_batched.csv)
     // eight (then four) slab loads in flight per step, summed in split order (the same sums as
     // four at a time: bit-identical; no measurable change in the step, profiles/r04/
     // splitk_reduce_depth_ab.txt)
@@ -624,8 +626,20 @@ __device__ __forceinline__ void reduce_outputs(const GemmParams& p, int b, int m
   const int b0 = b / p.batch1, b1 = b % p.batch1;
   if (p.n_dbias > 0 && n == 0 && p.dbias_tab[b0]) {   // the A row sums' split partials
     const float* src = p.dbias_ws + (int64_t)b * p.M + m;
+    const int64_t ts = (int64_t)nb * p.M;
     float r = 0.f;
-    for (int t = 0; t < p.splits; ++t) r += src[(int64_t)t * nb * p.M];
+    int t = 0;
+    // eight loads in flight per step, summed in split order (a plain loop issued them one at a
+    // time behind each add: ~20 dependent HBM round trips for the column-0 threads at 21 splits,
+    // the tail of every row-summing reduce launch)
+    for (; t + 8 <= p.splits; t += 8) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = src[(t + u) * ts];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) r += x[u];
+    }
+    for (; t < p.splits; ++t) r += src[t * ts];
     float* d = p.dbias_tab[b0];
     d[m] = (p.dbias_acc ? d[m] : 0.f) + r;
   }
