@@ -149,6 +149,28 @@ template <typename H> struct V4h {
 template <> struct V4<__bf16> : V4h<__bf16> {};
 template <> struct V4<_Float16> : V4h<_Float16> {};
 
+// 8 consecutive 16-bit values <-> one 16-B access, as two 4-element halves
+template <typename H>
+__device__ __forceinline__ void ld8(const H* p, float (&a)[4], float (&b)[4]) {
+  const uint4 t = *(const uint4*)p;
+  const H* h = (const H*)&t;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] = (float)h[e];
+    b[e] = (float)h[4 + e];
+  }
+}
+template <typename H>
+__device__ __forceinline__ void st8(H* p, const float (&a)[4], const float (&b)[4]) {
+  H h[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = (H)a[e];
+    h[4 + e] = (H)b[e];
+  }
+  *(uint4*)p = *(const uint4*)h;
+}
+
 template <typename TX, typename TY, int NV>
 __global__ __launch_bounds__(RB) void l2norm_fwd_vec_kernel(int64_t rows, const TX* x,
                                                             int64_t ldx, TY* y, int64_t ldy,
@@ -295,9 +317,11 @@ __global__ __launch_bounds__(RB) void ln_fwd_vec_kernel(int64_t rows, const TI* 
   }
 }
 
-// NV = D / 256: lane owns elements 4*(lane + 64 j) .. +3, j < NV
+// NV = D / 256: lane owns elements 4*(lane + 64 j) .. +3, j < NV.  C8 (D = 512, 16-bit x / r /
+// dy / dx with 16-B aligned rows): lane owns the 8 consecutive elements 8 lane .. +7 instead, one
+// 16-B access per row and operand (half the load / store instructions of the 8-B form)
 template <typename TI, typename TG, typename TD, int NV, bool DS = false,
-          int RPB = LN_ROWS_PER_BLOCK, int U = 1>
+          int RPB = LN_ROWS_PER_BLOCK, int U = 1, bool C8 = false>
 __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* x, int64_t ldx,
                                                         const TI* rr, int64_t ldr, const TG* dy,
                                                         int64_t lddy, const float* mean,
@@ -318,12 +342,16 @@ __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* 
     gamma = grp.gamma[gi];
     partials += (int64_t)gi * gridDim.x * NS * D;
   }
+  static_assert(!C8 || (NV == 2 && sizeof(TI) == 2 && sizeof(TG) == 2 && sizeof(TD) == 2),
+                "C8: D = 512, 16-bit operands");
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
+  // first element of the lane's j-th group of 4
+  auto col = [&](int j) { return C8 ? 8 * lane + 4 * j : 4 * (lane + 64 * j); };
   float pg[NV][4], pb[NV][4], gm[NV][4], ps[NV][4];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    const float4 g4 = *(const float4*)(gamma + 4 * (lane + 64 * j));
+    const float4 g4 = *(const float4*)(gamma + col(j));
     gm[j][0] = g4.x; gm[j][1] = g4.y; gm[j][2] = g4.z; gm[j][3] = g4.w;
 #pragma unroll
     for (int e = 0; e < 4; ++e) pg[j][e] = pb[j][e] = ps[j][e] = 0.f;
@@ -344,6 +372,21 @@ __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* 
       rw[u] = rc;
       mu[u] = mean[rc];
       rs[u] = rstd[rc];
+      if constexpr (C8) {
+        const int c = 8 * lane;
+        ld8(x + rc * ldx + c, xv[u][0], xv[u][1]);
+        if (rr) {
+          float r0[4], r1[4];
+          ld8(rr + rc * ldr + c, r0, r1);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            xv[u][0][e] += r0[e];
+            xv[u][1][e] += r1[e];
+          }
+        }
+        ld8(dy + rc * lddy + c, gv[u][0], gv[u][1]);
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < NV; ++j) {
         const int c = 4 * (lane + 64 * j);
@@ -377,26 +420,27 @@ __global__ __launch_bounds__(RB) void ln_bwd_vec_kernel(int64_t rows, const TI* 
       }
       s1 = wave_sum(s1) * (1.f / D);
       s2 = wave_sum(s2) * (1.f / D);
+      float o[NV][4];
 #pragma unroll
       for (int j = 0; j < NV; ++j) {
-        float o[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = rs[u] * (gd[j][e] - s1 - xh[j][e] * s2);
-        V4<TD>::st(dx + r * lddx + 4 * (lane + 64 * j), o);
+        for (int e = 0; e < 4; ++e) o[j][e] = rs[u] * (gd[j][e] - s1 - xh[j][e] * s2);
+        if constexpr (!C8) V4<TD>::st(dx + r * lddx + 4 * (lane + 64 * j), o[j]);
         if constexpr (DS) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) ps[j][e] += o[e];
+          for (int e = 0; e < 4; ++e) ps[j][e] += o[j][e];
         }
       }
+      if constexpr (C8) st8(dx + r * lddx + 8 * lane, o[0], o[1]);
     }
   }
 #pragma unroll
   for (int j = 0; j < NV; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      red[w][0][4 * (lane + 64 * j) + e] = pg[j][e];
-      red[w][1][4 * (lane + 64 * j) + e] = pb[j][e];
-      if constexpr (DS) red[w][2][4 * (lane + 64 * j) + e] = ps[j][e];
+      red[w][0][col(j) + e] = pg[j][e];
+      red[w][1][col(j) + e] = pb[j][e];
+      if constexpr (DS) red[w][2][col(j) + e] = ps[j][e];
     }
   __syncthreads();
   float* out = partials + (int64_t)blockIdx.x * NS * D;
@@ -848,6 +892,28 @@ extern "C" int jmt_layernorm_bwd_grouped_blocks(int64_t rows) {
   return (int)((rows + LN_ROWS_PER_BLOCK_GROUPED - 1) / LN_ROWS_PER_BLOCK_GROUPED);
 }
 
+// JMT_LN_C8=0: the LayerNorm backward keeps the 8-B element mapping (A/B switch)
+static bool ln_c8_off() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("JMT_LN_C8");
+    v = e ? atoi(e) : 1;
+  }
+  return v == 0;
+}
+
+// the C8 form of ln_bwd_vec_kernel applies: D = 512, 16-bit x / r / dy / dx of one type, 16-B
+// aligned bases, row (and group) strides multiples of 8 elements
+static bool ln_c8_ok(int dt_in, int dt_dy, int dt_dx, int D, const void* x, int64_t ldx,
+                     const void* r, int64_t ldr, const void* dy, int64_t lddy, const void* dx,
+                     int64_t lddx, int64_t sx = 0, int64_t sr = 0, int64_t sdy = 0,
+                     int64_t sdx = 0) {
+  return D == 512 && dt_in != JMT_F32 && dt_in == dt_dy && dt_in == dt_dx && !ln_c8_off() &&
+         ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
+         ldx % 8 == 0 && lddy % 8 == 0 && lddx % 8 == 0 && sx % 8 == 0 && sdy % 8 == 0 &&
+         sdx % 8 == 0 && (!r || (((uintptr_t)r & 15) == 0 && ldr % 8 == 0 && sr % 8 == 0));
+}
+
 extern "C" int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, int D,
                                  const void* x, int64_t ldx, const void* r, int64_t ldr,
                                  const void* dy, int64_t lddy, const float* mean,
@@ -870,7 +936,18 @@ extern "C" int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, 
   hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV>), dim3(nblk), dim3(RB), 0, st, rows, \
                      (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd, \
                      gamma, (TD*)dx, lddx, partials)
+  const bool c8 = vec && ln_c8_ok(dt_in, dt_dy, dt_dx, D, x, ldx, r, ldr, dy, lddy, dx, lddx);
   JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_dy, TG, JMT_DISPATCH1(dt_dx, TD,
+      constexpr bool same = sizeof(TI) == 2 && std::is_same<TI, TG>::value &&
+                            std::is_same<TI, TD>::value;
+      if constexpr (same) {
+        if (c8) {
+          hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, 2, false, LN_ROWS_PER_BLOCK, 1, true>),
+                             dim3(nblk), dim3(RB), 0, st, rows, (const TI*)x, ldx, (const TI*)r,
+                             ldr, (const TG*)dy, lddy, mean, rstd, gamma, (TD*)dx, lddx, partials);
+          break;
+        }
+      }
       if (vec && D == 512) { JMT_LNB_VEC(2); }
       else if (vec && D == 768) { JMT_LNB_VEC(3); }
       else if (vec && D == 1024) { JMT_LNB_VEC(4); }
@@ -910,7 +987,18 @@ extern "C" int jmt_layernorm_bwd_dsum(int dt_in, int dt_dy, int dt_dx, int64_t r
   hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, NV, true>), dim3(nblk), dim3(RB), 0, st, rows, \
                      (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd,    \
                      gamma, (TD*)dx, lddx, partials)
+  const bool c8 = ln_c8_ok(dt_in, dt_dy, dt_dx, D, x, ldx, r, ldr, dy, lddy, dx, lddx);
   JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_dy, TG, JMT_DISPATCH1(dt_dx, TD,
+      constexpr bool same = sizeof(TI) == 2 && std::is_same<TI, TG>::value &&
+                            std::is_same<TI, TD>::value;
+      if constexpr (same) {
+        if (c8) {
+          hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, 2, true, LN_ROWS_PER_BLOCK, 1, true>),
+                             dim3(nblk), dim3(RB), 0, st, rows, (const TI*)x, ldx, (const TI*)r,
+                             ldr, (const TG*)dy, lddy, mean, rstd, gamma, (TD*)dx, lddx, partials);
+          break;
+        }
+      }
       if (D == 512) { JMT_LNB_DS(2); }
       else if (D == 768) { JMT_LNB_DS(3); }
       else { JMT_LNB_DS(4); })));
@@ -1134,11 +1222,25 @@ extern "C" int jmt_layernorm_bwd_grouped(int dt_in, int dt_dy, int dt_dx, int G,
                      dim3(RB), 0, st, rows,                                                     \
                      (const TI*)x, ldx, (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd,     \
                      grp.gamma[0], (TD*)dx, lddx, partials, grp)
+  // 16-B rows for the C8 form (D = 512): every base 16-B aligned, every stride a multiple of 8
+  const bool c8 = ln_c8_ok(dt_in, dt_dy, dt_dx, D, x, ldx, r, ldr, dy, lddy, dx, lddx, sx, sr,
+                           sdy, sdx);
+#define JMT_LNBG_C8(DS)                                                                          \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<TI, TG, TD, 2, DS, LN_ROWS_PER_BLOCK_GROUPED, 2,         \
+                                        true>), grid, dim3(RB), 0, st, rows, (const TI*)x, ldx,  \
+                     (const TI*)r, ldr, (const TG*)dy, lddy, mean, rstd, grp.gamma[0], (TD*)dx,  \
+                     lddx, partials, grp)
 #define JMT_LNBG(NV, DS) JMT_LNBG_U(NV, DS, 2)
   JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_dy, TG, JMT_DISPATCH1(dt_dx, TD,
       constexpr bool same = sizeof(TI) == 2 && std::is_same<TI, TG>::value &&
                             std::is_same<TI, TD>::value;
       (void)same;
+      if constexpr (same) {
+        if (c8) {
+          if (dsum) { JMT_LNBG_C8(true); } else { JMT_LNBG_C8(false); }
+          break;
+        }
+      }
       if (dsum) {
         if (D == 512) { JMT_LNBG(2, true); }
         else if (D == 768) { JMT_LNBG(3, true); }
@@ -1148,6 +1250,7 @@ extern "C" int jmt_layernorm_bwd_grouped(int dt_in, int dt_dy, int dt_dx, int G,
         else if (D == 768) { JMT_LNBG(3, false); }
         else { JMT_LNBG(4, false); }
       })));
+#undef JMT_LNBG_C8
 #undef JMT_LNBG
 #undef JMT_LNBG_U
   JMT_LAUNCH_CHECK("jmt_layernorm_bwd_grouped");

@@ -467,6 +467,52 @@ def test_add_layernorm_fwd_bwd(cd, D):
     assert (bet.grad - b2.grad).abs().max().item() <= tol * b2.grad.abs().max().item()
 
 
+@pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
+def test_layernorm_bwd_16b_rows_match_8b_rows(cd):
+    """Round 6: at D = 512 with 16-bit operands and 16-B aligned rows the LayerNorm backward
+    maps 8 consecutive elements to a lane (one 16-B access per row and operand); rows whose
+    stride is only a multiple of 4 (here 516) keep the 8-B mapping.  Same data through both:
+    dgamma / dbeta bit-identical (same row order per element), dx within one rounding of the
+    compute dtype (the row sums s1, s2 reassociate), both vs torch fp32."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    rows, D = 1000, 512
+    X = (torch.randn(rows, D, device=DEV, generator=g) * 2 + 0.5).to(cd)
+    R = torch.randn(rows, D, device=DEV, generator=g).to(cd)
+    dY = torch.randn(rows, D, device=DEV, generator=g).to(cd)
+    gam = 1 + 0.1 * torch.randn(D, device=DEV, generator=g)
+    bet = 0.1 * torch.randn(D, device=DEV, generator=g)
+
+    def padded(t):
+        b = torch.zeros(rows, D + 4, device=DEV, dtype=t.dtype)
+        b[:, :D] = t
+        return b
+
+    Y = torch.empty_like(X)
+    st = torch.empty(2, rows, device=DEV)
+    ops.layernorm_fwd(X, D, R, D, gam, bet, 1e-5, Y, D, st[0], st[1], rows, D)
+    outs = []
+    for pad in (False, True):
+        x, r, dy = (padded(t) if pad else t for t in (X, R, dY))
+        ld = D + 4 if pad else D
+        dx = torch.zeros(rows, ld, device=DEV, dtype=cd)
+        dg = torch.zeros(D, device=DEV)
+        db = torch.zeros(D, device=DEV)
+        ops.layernorm_bwd(x, ld, r, ld, dy, ld, st[0], st[1], gam, dx, ld, dg, db, True, rows, D)
+        torch.cuda.synchronize()
+        outs.append((dx[:, :D].clone(), dg, db))
+    (a, b) = outs
+    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    xr = (X.float() + R.float()).requires_grad_(True)
+    g2 = gam.clone().requires_grad_(True)
+    b2 = bet.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr, (D,), g2, b2, 1e-5).backward(dY.float())
+    scale = xr.grad.abs().max().item()
+    for dx, dg, _ in outs:
+        assert (dx.float() - xr.grad).abs().max().item() <= 2e-2 * scale
+        assert (dg - g2.grad).abs().max().item() <= 2e-2 * g2.grad.abs().max().item()
+    assert (a[0].float() - b[0].float()).abs().max().item() <= 1e-2 * scale
+
+
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("H,Lq,Lk,N", [(1, 300, 300, 3), (8, 37, 37, 2), (1, 1, 6, 40),
                                        (4, 64, 17, 5)])
