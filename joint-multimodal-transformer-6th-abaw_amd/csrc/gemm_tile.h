@@ -592,6 +592,8 @@ __device__ __forceinline__ void reduce_outputs(const GemmParams& p, int b, int m
   if constexpr (W == 4) {
     // (every slab load of up to 32 splits issued before the first add measured slower: 19.7 vs
     // 17.3 us per reduce launch in the c3 step, profiles/r06/reduce_prof_all_loads_first.csv vs reduce_prof_rowsum_batched.csv)
+    // (two lanes per output group, each summing half of the splits, then lo + hi: slower in
+    // the c3 step, 4.014-4.024 vs 4.001-4.011 ms, profiles/r06/step_ab_skr_pair.txt)
     // eight (then four) slab loads in flight per step, summed in split order (the same sums as
     // four at a time: bit-identical; no measurable change in the step, profiles/r04/
     // splitk_reduce_depth_ab.txt)
