@@ -245,10 +245,8 @@ struct LnGrp {
 
 // Vector forward (D = 256 NV, 4-aligned rows): lane owns elements 4*(lane + 64 j) .. +3; each
 // wave normalises LNF_RPW rows, issuing all of a row's x / residual loads before its reductions.
-// C8 (D = 512, 16-bit x / r / y with 16-B aligned rows): lane owns 8 consecutive elements,
-// 8 lane .. +7 (one 16-B access per row and operand), as in ln_bwd_vec_kernel.
 constexpr int LNF_RPW = 4;
-template <typename TI, typename TO, int NV, bool C8 = false>
+template <typename TI, typename TO, int NV>
 __global__ __launch_bounds__(RB) void ln_fwd_vec_kernel(int64_t rows, const TI* x, int64_t ldx,
                                                         const TI* rr, int64_t ldr,
                                                         const float* gamma, const float* beta,
@@ -267,43 +265,28 @@ __global__ __launch_bounds__(RB) void ln_fwd_vec_kernel(int64_t rows, const TI* 
     gamma = grp.gamma[gi];
     beta = grp.beta[gi];
   }
-  static_assert(!C8 || (NV == 2 && sizeof(TI) == 2 && sizeof(TO) == 2), "C8: D = 512, 16-bit");
   const int lane = threadIdx.x & 63;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LNF_RPW;
-  auto col = [&](int j) { return C8 ? 8 * lane + 4 * j : 4 * (lane + 64 * j); };
   float gm[NV][4], bt[NV][4];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    V4<float>::ld(gamma + col(j), gm[j]);
-    V4<float>::ld(beta + col(j), bt[j]);
+    V4<float>::ld(gamma + 4 * (lane + 64 * j), gm[j]);
+    V4<float>::ld(beta + 4 * (lane + 64 * j), bt[j]);
   }
   for (int i = 0; i < LNF_RPW; ++i) {
     const int64_t r = r0 + i;
     if (r >= rows) return;
     float v[NV][4];
     float s = 0.f;
-    if constexpr (C8) {
-      ld8(x + r * ldx + 8 * lane, v[0], v[1]);
-      if (rr) {
-        float t0[4], t1[4];
-        ld8(rr + r * ldr + 8 * lane, t0, t1);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[0][e] += t0[e];
-          v[1][e] += t1[e];
-        }
-      }
-    } else {
+    for (int j = 0; j < NV; ++j) V4<TI>::ld(x + r * ldx + 4 * (lane + 64 * j), v[j]);
+    if (rr) {
 #pragma unroll
-      for (int j = 0; j < NV; ++j) V4<TI>::ld(x + r * ldx + 4 * (lane + 64 * j), v[j]);
-      if (rr) {
+      for (int j = 0; j < NV; ++j) {
+        float t[4];
+        V4<TI>::ld(rr + r * ldr + 4 * (lane + 64 * j), t);
 #pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          float t[4];
-          V4<TI>::ld(rr + r * ldr + 4 * (lane + 64 * j), t);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[j][e] += t[e];
-        }
+        for (int e = 0; e < 4; ++e) v[j][e] += t[e];
       }
     }
 #pragma unroll
@@ -322,11 +305,11 @@ __global__ __launch_bounds__(RB) void ln_fwd_vec_kernel(int64_t rows, const TI* 
     const float rs = rsqrtf(wave_sum(q) * (1.f / D) + eps);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
+      float o[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[j][e] = (v[j][e] - mu) * rs * gm[j][e] + bt[j][e];
-      if constexpr (!C8) V4<TO>::st(y + r * ldy + 4 * (lane + 64 * j), v[j]);
+      for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mu) * rs * gm[j][e] + bt[j][e];
+      V4<TO>::st(y + r * ldy + 4 * (lane + 64 * j), o);
     }
-    if constexpr (C8) st8(y + r * ldy + 8 * lane, v[0], v[1]);
     if (lane == 0) {
       mean[r] = mu;
       rstd[r] = rs;
@@ -870,28 +853,6 @@ extern "C" int jmt_l2norm_bwd(int x_dt, int dy_dt, int dx_dt, int64_t rows, int 
   return JMT_OK;
 }
 
-// JMT_LN_C8=0: the LayerNorm forward / backward keep the 8-B element mapping (A/B switch)
-static bool ln_c8_off() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("JMT_LN_C8");
-    v = e ? atoi(e) : 1;
-  }
-  return v == 0;
-}
-
-// the C8 form of ln_bwd_vec_kernel applies: D = 512, 16-bit x / r / dy / dx of one type, 16-B
-// aligned bases, row (and group) strides multiples of 8 elements
-static bool ln_c8_ok(int dt_in, int dt_dy, int dt_dx, int D, const void* x, int64_t ldx,
-                     const void* r, int64_t ldr, const void* dy, int64_t lddy, const void* dx,
-                     int64_t lddx, int64_t sx = 0, int64_t sr = 0, int64_t sdy = 0,
-                     int64_t sdx = 0) {
-  return D == 512 && dt_in != JMT_F32 && dt_in == dt_dy && dt_in == dt_dx && !ln_c8_off() &&
-         ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
-         ldx % 8 == 0 && lddy % 8 == 0 && lddx % 8 == 0 && sx % 8 == 0 && sdy % 8 == 0 &&
-         sdx % 8 == 0 && (!r || (((uintptr_t)r & 15) == 0 && ldr % 8 == 0 && sr % 8 == 0));
-}
-
 extern "C" int jmt_layernorm_fwd(int dt_in, int dt_out, int64_t rows, int D, const void* x,
                                  int64_t ldx, const void* r, int64_t ldr, const float* gamma,
                                  const float* beta, float eps, void* y, int64_t ldy, float* mean,
@@ -909,16 +870,7 @@ extern "C" int jmt_layernorm_fwd(int dt_in, int dt_out, int64_t rows, int D, con
   hipLaunchKernelGGL((ln_fwd_vec_kernel<TI, TO, NV>), dim3(vblocks), dim3(RB), 0, st, rows, \
                      (const TI*)x, ldx, (const TI*)r, ldr, gamma, beta, eps, (TO*)y, ldy, mean, \
                      rstd)
-  const bool c8 = vec && ln_c8_ok(dt_in, dt_in, dt_out, D, x, ldx, r, ldr, x, ldx, y, ldy);
   JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_out, TO,
-      if constexpr (sizeof(TI) == 2 && std::is_same<TI, TO>::value) {
-        if (c8) {
-          hipLaunchKernelGGL((ln_fwd_vec_kernel<TI, TO, 2, true>), dim3(vblocks), dim3(RB), 0, st,
-                             rows, (const TI*)x, ldx, (const TI*)r, ldr, gamma, beta, eps, (TO*)y,
-                             ldy, mean, rstd);
-          break;
-        }
-      }
       if (vec && D == 512) { JMT_LNF_VEC(2); }
       else if (vec && D == 768) { JMT_LNF_VEC(3); }
       else if (vec && D == 1024) { JMT_LNF_VEC(4); }
@@ -938,6 +890,28 @@ extern "C" int jmt_layernorm_bwd_blocks(int64_t rows) {
 
 extern "C" int jmt_layernorm_bwd_grouped_blocks(int64_t rows) {
   return (int)((rows + LN_ROWS_PER_BLOCK_GROUPED - 1) / LN_ROWS_PER_BLOCK_GROUPED);
+}
+
+// JMT_LN_C8=0: the LayerNorm backward keeps the 8-B element mapping (A/B switch)
+static bool ln_c8_off() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("JMT_LN_C8");
+    v = e ? atoi(e) : 1;
+  }
+  return v == 0;
+}
+
+// the C8 form of ln_bwd_vec_kernel applies: D = 512, 16-bit x / r / dy / dx of one type, 16-B
+// aligned bases, row (and group) strides multiples of 8 elements
+static bool ln_c8_ok(int dt_in, int dt_dy, int dt_dx, int D, const void* x, int64_t ldx,
+                     const void* r, int64_t ldr, const void* dy, int64_t lddy, const void* dx,
+                     int64_t lddx, int64_t sx = 0, int64_t sr = 0, int64_t sdy = 0,
+                     int64_t sdx = 0) {
+  return D == 512 && dt_in != JMT_F32 && dt_in == dt_dy && dt_in == dt_dx && !ln_c8_off() &&
+         ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
+         ldx % 8 == 0 && lddy % 8 == 0 && lddx % 8 == 0 && sx % 8 == 0 && sdy % 8 == 0 &&
+         sdx % 8 == 0 && (!r || (((uintptr_t)r & 15) == 0 && ldr % 8 == 0 && sr % 8 == 0));
 }
 
 extern "C" int jmt_layernorm_bwd(int dt_in, int dt_dy, int dt_dx, int64_t rows, int D,
@@ -1203,17 +1177,7 @@ extern "C" int jmt_layernorm_fwd_grouped(int dt_in, int dt_out, int G, int64_t r
   hipLaunchKernelGGL((ln_fwd_vec_kernel<TI, TO, NV>), grid, dim3(RB), 0, st, rows, (const TI*)x, \
                      ldx, (const TI*)r, ldr, grp.gamma[0], grp.beta[0], eps, (TO*)y, ldy, mean,  \
                      rstd, grp)
-  const bool c8 = ln_c8_ok(dt_in, dt_in, dt_out, D, x, ldx, r, ldr, x, ldx, y, ldy, sx, sr, sx,
-                           sy);
   JMT_DISPATCH1(dt_in, TI, JMT_DISPATCH1(dt_out, TO,
-      if constexpr (sizeof(TI) == 2 && std::is_same<TI, TO>::value) {
-        if (c8) {
-          hipLaunchKernelGGL((ln_fwd_vec_kernel<TI, TO, 2, true>), grid, dim3(RB), 0, st, rows,
-                             (const TI*)x, ldx, (const TI*)r, ldr, grp.gamma[0], grp.beta[0], eps,
-                             (TO*)y, ldy, mean, rstd, grp);
-          break;
-        }
-      }
       if (D == 512) { JMT_LNFG(2); }
       else if (D == 768) { JMT_LNFG(3); }
       else { JMT_LNFG(4); }));

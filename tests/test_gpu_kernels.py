@@ -469,8 +469,7 @@ def test_add_layernorm_fwd_bwd(cd, D):
 
 @pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
 def test_layernorm_bwd_16b_rows_match_8b_rows(cd):
-    """Round 6: at D = 512 with 16-bit operands and 16-B aligned rows the LayerNorm forward and
-    backward
+    """Round 6: at D = 512 with 16-bit operands and 16-B aligned rows the LayerNorm backward
     maps 8 consecutive elements to a lane (one 16-B access per row and operand); rows whose
     stride is only a multiple of 4 (here 516) keep the 8-B mapping.  Same data through both:
     dgamma / dbeta bit-identical (same row order per element), dx within one rounding of the
@@ -491,17 +490,6 @@ def test_layernorm_bwd_16b_rows_match_8b_rows(cd):
     Y = torch.empty_like(X)
     st = torch.empty(2, rows, device=DEV)
     ops.layernorm_fwd(X, D, R, D, gam, bet, 1e-5, Y, D, st[0], st[1], rows, D)
-    # the forward takes the same two mappings (16-B rows here, 8-B on the padded copy)
-    Yp = torch.zeros(rows, D + 4, device=DEV, dtype=cd)
-    stp = torch.empty(2, rows, device=DEV)
-    ops.layernorm_fwd(padded(X), D + 4, padded(R), D + 4, gam, bet, 1e-5, Yp, D + 4, stp[0],
-                      stp[1], rows, D)
-    torch.cuda.synchronize()
-    yref = torch.nn.functional.layer_norm(X.float() + R.float(), (D,), gam, bet, 1e-5)
-    for y in (Y, Yp[:, :D]):
-        assert (y.float() - yref).abs().max().item() <= 2e-2 * yref.abs().max().item()
-    assert (Y.float() - Yp[:, :D].float()).abs().max().item() <= 1e-2 * yref.abs().max().item()
-    assert torch.allclose(st, stp, rtol=1e-5, atol=1e-6)
     outs = []
     for pad in (False, True):
         x, r, dy = (padded(t) if pad else t for t in (X, R, dY))
